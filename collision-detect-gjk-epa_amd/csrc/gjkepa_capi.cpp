@@ -1,0 +1,243 @@
+// gjkepa_capi.cpp — the C-ABI of include/gjkepa.h over the tiered HIP kernels.
+//
+// Host-buffer entries (gjkepa_query, gjkepa_batch) own per-device staging buffers that grow as
+// needed and are reused; they are serialised per device by a mutex, so concurrent callers (the
+// reference's `!$OMP PARALLEL DO ... CALL GJKEPA` pattern) are safe.  gjkepa_batch_device never
+// allocates or synchronises: it enqueues one hipMemsetAsync and three kernels on the stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gjkepa.h"
+#include "gjkepa_kernel.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(GJKEPA_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr int64_t kWsHeader = 256;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 4096;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+
+struct DeviceState {
+    std::mutex mu;
+    bool init = false;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    DevBuf verts, off, cnt, pairs, out, ws;
+};
+
+std::mutex g_table_mu;
+std::vector<DeviceState*> g_dev;
+
+DeviceState* device_state(int device, int* rc) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) { *rc = fail(GJKEPA_E_NODEVICE, "no HIP device"); return nullptr; }
+    if (device < 0 || device >= n) { *rc = fail(GJKEPA_E_ARG, "device index out of range"); return nullptr; }
+    std::lock_guard<std::mutex> g(g_table_mu);
+    if ((int)g_dev.size() < n) g_dev.resize((size_t)n, nullptr);
+    if (!g_dev[(size_t)device]) g_dev[(size_t)device] = new DeviceState();
+    *rc = 0;
+    return g_dev[(size_t)device];
+}
+
+int num_cus_current() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+    return cus;
+}
+
+int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
+            const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
+            void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus) {
+    if (n_pairs == 0) return 0;
+    if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
+    char* ws = (char*)workspace;
+    int32_t* counts = (int32_t*)ws;                      // [0] tier-1 list size, [1] tier-2 list size
+    int32_t* list1 = (int32_t*)(ws + kWsHeader);
+    int32_t* list2 = list1 + n_pairs;
+    hipError_t e = hipMemsetAsync(counts, 0, kWsHeader, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    gjkepa_tier_args a{};
+    a.version = version;
+    a.tol_ff = tol_ff;
+    a.verts = verts;
+    a.hull_off = hull_off;
+    a.hull_cnt = hull_cnt;
+    a.pairs = pairs;
+    a.n_pairs = n_pairs;
+    a.out = out;
+    a.num_cus = num_cus;
+    a.grid = 0;
+    // tier 0: every pair
+    a.in_list = nullptr; a.in_count = nullptr; a.out_list = list1; a.out_count = counts + 0;
+    e = gjkepa_launch_tier(0, vert_dtype, precision, a, s);
+    if (e != hipSuccess) return hip_fail(e, "tier 0 launch");
+    // tier 1: pairs deferred by tier 0
+    a.in_list = list1; a.in_count = counts + 0; a.out_list = list2; a.out_count = counts + 1;
+    e = gjkepa_launch_tier(1, vert_dtype, precision, a, s);
+    if (e != hipSuccess) return hip_fail(e, "tier 1 launch");
+    // tier 2: worst-case capacities, never defers
+    a.in_list = list2; a.in_count = counts + 1; a.out_list = nullptr; a.out_count = nullptr;
+    e = gjkepa_launch_tier(2, vert_dtype, precision, a, s);
+    if (e != hipSuccess) return hip_fail(e, "tier 2 launch");
+    return 0;
+}
+
+bool valid_enums(int32_t vert_dtype, int32_t precision) {
+    return (vert_dtype == GJKEPA_DTYPE_F32 || vert_dtype == GJKEPA_DTYPE_F64) &&
+           (precision == GJKEPA_PREC_F32 || precision == GJKEPA_PREC_F64);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gjkepa_record_bytes(int32_t precision) {
+    if (precision == GJKEPA_PREC_F64) return (int)sizeof(gjkepa_contact_f64);
+    if (precision == GJKEPA_PREC_F32) return (int)sizeof(gjkepa_contact_f32);
+    return GJKEPA_E_ARG;
+}
+
+int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
+    if (n_pairs < 0) return GJKEPA_E_ARG;
+    return kWsHeader + 2 * (int64_t)sizeof(int32_t) * n_pairs;
+}
+
+const char* gjkepa_last_error(void) { return g_err.c_str(); }
+
+const char* gjkepa_version_string(void) {
+    static char buf[256];
+    std::snprintf(buf, sizeof(buf),
+                  "gjkepa-mi355x gfx950 wave64; tiers K/VCAP/FCAP = %d/%d/%d, %d/%d/%d, %d/%d/%d; "
+                  "-O3 -ffp-contract=off",
+                  GJKEPA_T0_K, GJKEPA_T0_VCAP, GJKEPA_T0_FCAP, GJKEPA_T1_K, GJKEPA_T1_VCAP, GJKEPA_T1_FCAP,
+                  GJKEPA_T2_K, GJKEPA_T2_VCAP, GJKEPA_T2_FCAP);
+    return buf;
+}
+
+int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                        const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                        const int32_t* pairs, int64_t n_pairs, void* out, void* workspace,
+                        int64_t workspace_bytes, void* stream) {
+    if (n_pairs < 0 || !valid_enums(vert_dtype, precision)) return fail(GJKEPA_E_ARG, "bad n_pairs/dtype/precision");
+    if (n_pairs > 0 && (!verts || !hull_off || !hull_cnt || !pairs || !out || !workspace))
+        return fail(GJKEPA_E_ARG, "null pointer");
+    if (n_pairs > INT32_MAX) return fail(GJKEPA_E_ARG, "n_pairs above 2^31-1");
+    return enqueue(version, tol_ff, vert_dtype, precision, verts, hull_off, hull_cnt, pairs, n_pairs, out,
+                   workspace, workspace_bytes, (hipStream_t)stream, num_cus_current());
+}
+
+int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                 const void* verts, int64_t n_vert_scalars, const int64_t* hull_off,
+                 const int32_t* hull_cnt, int64_t n_hulls, const int32_t* pairs, int64_t n_pairs,
+                 void* out, int32_t device) {
+    if (n_pairs < 0 || n_hulls < 0 || n_vert_scalars < 0 || !valid_enums(vert_dtype, precision))
+        return fail(GJKEPA_E_ARG, "bad sizes/dtype/precision");
+    if (n_pairs == 0) return 0;
+    if (!verts || !hull_off || !hull_cnt || !pairs || !out) return fail(GJKEPA_E_ARG, "null pointer");
+    if (n_pairs > INT32_MAX) return fail(GJKEPA_E_ARG, "n_pairs above 2^31-1");
+    // host-side validation of the index structure (device code trusts it)
+    for (int64_t k = 0; k < 2 * n_pairs; ++k)
+        if (pairs[k] < 0 || pairs[k] >= n_hulls) return fail(GJKEPA_E_ARG, "pair references a missing hull");
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        int64_t c = hull_cnt[h];
+        if (c >= 1 && (hull_off[h] < 0 || hull_off[h] + 3 * c > n_vert_scalars))
+            return fail(GJKEPA_E_ARG, "hull outside the vertex pool");
+    }
+    int rc = 0;
+    DeviceState* d = device_state(device, &rc);
+    if (!d) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (!d->init) {
+        e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        d->num_cus = num_cus_current();
+        d->init = true;
+    }
+    const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
+    const size_t rec = (size_t)gjkepa_record_bytes(precision);
+    if ((e = d->verts.ensure((size_t)n_vert_scalars * esz)) != hipSuccess ||
+        (e = d->off.ensure((size_t)n_hulls * 8)) != hipSuccess ||
+        (e = d->cnt.ensure((size_t)n_hulls * 4)) != hipSuccess ||
+        (e = d->pairs.ensure((size_t)n_pairs * 8)) != hipSuccess ||
+        (e = d->out.ensure((size_t)n_pairs * rec)) != hipSuccess ||
+        (e = d->ws.ensure((size_t)gjkepa_workspace_bytes(n_pairs))) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    hipStream_t s = d->stream;
+    if ((e = hipMemcpyAsync(d->verts.p, verts, (size_t)n_vert_scalars * esz, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->off.p, hull_off, (size_t)n_hulls * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->cnt.p, hull_cnt, (size_t)n_hulls * 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->pairs.p, pairs, (size_t)n_pairs * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    rc = enqueue(version, tol_ff, vert_dtype, precision, d->verts.p, (const int64_t*)d->off.p,
+                 (const int32_t*)d->cnt.p, (const int32_t*)d->pairs.p, n_pairs, d->out.p, d->ws.p,
+                 (int64_t)d->ws.cap, s, d->num_cus);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(out, d->out.p, (size_t)n_pairs * rec, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, const double* p2, int32_t n2,
+                 int8_t* collision, int32_t* colli_type, double* nearest_points, double* collision_normal,
+                 double* collision_point, double* penetration_depth, int32_t* status, int32_t device) {
+    if (!p1 || !p2 || !collision || !colli_type || !nearest_points || !collision_normal || !collision_point ||
+        !penetration_depth)
+        return fail(GJKEPA_E_ARG, "null pointer");
+    if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
+    std::vector<double> pool((size_t)3 * (size_t)(n1 + n2) + 1, 0.0);
+    std::memcpy(pool.data(), p1, sizeof(double) * 3 * (size_t)n1);
+    std::memcpy(pool.data() + 3 * (size_t)n1, p2, sizeof(double) * 3 * (size_t)n2);
+    int64_t off[2] = {0, 3 * (int64_t)n1};
+    int32_t cnt[2] = {n1, n2};
+    int32_t pr[2] = {0, 1};
+    gjkepa_contact_f64 r;
+    int rc = gjkepa_batch(version, tol_ff, GJKEPA_DTYPE_F64, GJKEPA_PREC_F64, pool.data(), (int64_t)pool.size(),
+                          off, cnt, 2, pr, 1, &r, device);
+    if (rc) return rc;
+    *collision = r.collision;
+    *colli_type = r.colli_type;
+    // nearest_points_(2,3), Fortran column-major: (1,k) = p1, (2,k) = p2
+    for (int k = 0; k < 3; ++k) {
+        nearest_points[2 * k] = r.nearest_points[k];
+        nearest_points[2 * k + 1] = r.nearest_points[3 + k];
+        collision_normal[k] = r.collision_normal[k];
+        collision_point[k] = r.collision_point[k];
+    }
+    *penetration_depth = r.penetration_depth;
+    if (status) *status = r.status;
+    return 0;
+}
+
+}  // extern "C"

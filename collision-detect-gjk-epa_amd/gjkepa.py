@@ -1,0 +1,216 @@
+"""Python host binding of the MI355X GJK/EPA C-ABI (include/gjkepa.h) via ctypes.
+
+Mirrors the reference's operator interface: ``gjkepa(version, tol_ff, p1, p2)`` answers one
+pair exactly like ``CALL GJKEPA(version_, TOL_FF_, p1_, p2_, ...)`` in
+src/GCLIB_GJKEPA.f90:39-52 (same argument meaning; p1/p2 are (n, 3) vertex arrays) and returns
+the reference's INTENT(OUT) arguments.  ``gjkepa_batch`` runs a pooled hull set; the
+``*_device`` form takes device pointers (e.g. torch tensors on cuda) and an optional stream.
+
+There is no CPU fallback: importing works without a GPU (so the library can be inspected),
+but every compute call goes to libgjkepa_hip.so and fails loudly if it cannot run.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libgjkepa_hip.so")
+FLIB_PATH = os.path.join(_HERE, "build", "libgclib_gjkepa.so")
+
+STATUS_OK, STATUS_EPA_MAXITER, STATUS_DEGENERATE, STATUS_BAD_VERSION, STATUS_BAD_INPUT = 0, 1, 2, 3, 4
+DTYPE_F32, DTYPE_F64 = 0, 1
+PREC_F32, PREC_F64 = 0, 1
+MAX_HULL_VERTS = 256
+
+# exported symbols declared in include/gjkepa.h
+EXPORTS = (
+    "gjkepa_record_bytes", "gjkepa_query", "gjkepa_batch", "gjkepa_workspace_bytes",
+    "gjkepa_batch_device", "gjkepa_last_error", "gjkepa_version_string", "gjkepa_synth_pairs",
+)
+
+REC64 = np.dtype([
+    ("penetration_depth", "<f8"), ("collision_normal", "<f8", (3,)), ("collision_point", "<f8", (3,)),
+    ("nearest_points", "<f8", (6,)), ("collision", "i1"), ("colli_type", "i1"), ("status", "i1"),
+    ("reserved", "i1"), ("diag", "<u4"), ("pad", "<u4", (4,)),
+])
+REC32 = np.dtype([
+    ("penetration_depth", "<f4"), ("collision_normal", "<f4", (3,)), ("collision_point", "<f4", (3,)),
+    ("nearest_points", "<f4", (6,)), ("collision", "i1"), ("colli_type", "i1"), ("status", "i1"),
+    ("reserved", "i1"), ("diag", "<u4"), ("pad", "<u4"),
+])
+assert REC64.itemsize == 128 and REC32.itemsize == 64
+
+
+def record_dtype(precision: int) -> np.dtype:
+    return REC64 if precision == PREC_F64 else REC32
+
+
+_lib = None
+
+
+class GjkEpaError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libgjkepa_hip.so (built in-tree by ``make`` / __graft_entry__.build())."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GjkEpaError(f"{p} not built; run `make -C collision-detect-gjk-epa_amd`")
+    lib = ctypes.CDLL(p)
+    c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+    lib.gjkepa_record_bytes.argtypes = [c_i32]
+    lib.gjkepa_record_bytes.restype = ctypes.c_int
+    lib.gjkepa_workspace_bytes.argtypes = [c_i64]
+    lib.gjkepa_workspace_bytes.restype = c_i64
+    lib.gjkepa_last_error.restype = ctypes.c_char_p
+    lib.gjkepa_version_string.restype = ctypes.c_char_p
+    lib.gjkepa_query.argtypes = [c_i32, c_dbl, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32]
+    lib.gjkepa_query.restype = ctypes.c_int
+    lib.gjkepa_batch.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32]
+    lib.gjkepa_batch.restype = ctypes.c_int
+    lib.gjkepa_batch_device.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]
+    lib.gjkepa_batch_device.restype = ctypes.c_int
+    lib.gjkepa_synth_pairs.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp, c_vp]
+    lib.gjkepa_synth_pairs.restype = c_i64
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().gjkepa_last_error().decode(errors="replace")
+        raise GjkEpaError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+@dataclass
+class Contact:
+    """GJKEPA's INTENT(OUT) arguments (GCLIB_GJKEPA.f90:47-52) plus the status code."""
+    collision: bool
+    colli_type: int
+    nearest_points: np.ndarray     # (2, 3): row 0 on p1, row 1 on p2
+    collision_normal: np.ndarray   # (3,)
+    collision_point: np.ndarray    # (3,)
+    penetration_depth: float
+    status: int
+
+
+def gjkepa(version: int, tol_ff: float, p1, p2, device: int = 0) -> Contact:
+    """One pair on the GPU; same arguments as the reference GJKEPA (p1, p2: (n, 3))."""
+    lib = load()
+    a = np.ascontiguousarray(np.asarray(p1, dtype=np.float64).T)   # column-major (n,3) = x[], y[], z[]
+    b = np.ascontiguousarray(np.asarray(p2, dtype=np.float64).T)
+    hit = np.zeros(1, np.int8)
+    typ = np.zeros(1, np.int32)
+    st = np.zeros(1, np.int32)
+    npf = np.zeros(6)
+    nrm = np.zeros(3)
+    pt = np.zeros(3)
+    dep = np.zeros(1)
+    rc = lib.gjkepa_query(int(version), float(tol_ff), _ptr(a), a.shape[1], _ptr(b), b.shape[1],
+                          _ptr(hit), _ptr(typ), _ptr(npf), _ptr(nrm), _ptr(pt), _ptr(dep), _ptr(st), int(device))
+    _check(rc, "gjkepa_query")
+    return Contact(bool(hit[0]), int(typ[0]), npf.reshape(3, 2).T.copy(), nrm, pt, float(dep[0]), int(st[0]))
+
+
+@dataclass
+class HullPool:
+    """Pooled hulls: hull h = verts[off[h] : off[h] + 3*cnt[h]] as x[], y[], z[]."""
+    verts: np.ndarray    # float32 or float64
+    hull_off: np.ndarray  # int64
+    hull_cnt: np.ndarray  # int32
+    pairs: np.ndarray     # int32 (n_pairs, 2)
+
+    @property
+    def n_pairs(self) -> int:
+        return int(self.pairs.shape[0])
+
+    @property
+    def dtype_code(self) -> int:
+        return DTYPE_F32 if self.verts.dtype == np.float32 else DTYPE_F64
+
+    def hull(self, h: int) -> np.ndarray:
+        o, n = int(self.hull_off[h]), int(self.hull_cnt[h])
+        return self.verts[o:o + 3 * n].reshape(3, n).T.astype(np.float64)
+
+    def as_dtype(self, dt) -> "HullPool":
+        return HullPool(self.verts.astype(dt), self.hull_off, self.hull_cnt, self.pairs)
+
+    @staticmethod
+    def from_pairs(pairs_list, dtype=np.float64) -> "HullPool":
+        """Build a pool from a list of (p1, p2) (n,3) arrays."""
+        chunks, off, cnt, pr = [], [], [], []
+        o = 0
+        for k, (a, b) in enumerate(pairs_list):
+            for h in (a, b):
+                h = np.asarray(h, dtype=np.float64).reshape(-1, 3)
+                chunks.append(h.T.reshape(-1))
+                off.append(o)
+                cnt.append(h.shape[0])
+                o += 3 * h.shape[0]
+            pr.append((2 * k, 2 * k + 1))
+        verts = np.concatenate(chunks).astype(dtype) if chunks else np.zeros(0, dtype)
+        return HullPool(verts, np.asarray(off, np.int64), np.asarray(cnt, np.int32),
+                        np.asarray(pr, np.int32).reshape(-1, 2))
+
+
+def synth_pairs(seed: int, n_pairs: int, n_min: int = 32, n_max: int = 32, r_max: float = 2.5,
+                first_pair: int = 0, dtype=np.float32) -> HullPool:
+    """Deterministic synthetic workload: C2 = (32, 32, 2.5), C4 = (8, 256, 2.5),
+    C5 = (32..128, 0.3)."""
+    lib = load()
+    code = DTYPE_F32 if np.dtype(dtype) == np.float32 else DTYPE_F64
+    total = lib.gjkepa_synth_pairs(seed, first_pair, n_pairs, n_min, n_max, r_max, code, None, None, None, None)
+    if total < 0:
+        raise GjkEpaError("gjkepa_synth_pairs: bad arguments")
+    verts = np.empty(total, dtype=dtype)
+    off = np.empty(2 * n_pairs, np.int64)
+    cnt = np.empty(2 * n_pairs, np.int32)
+    prs = np.empty(2 * n_pairs, np.int32)
+    lib.gjkepa_synth_pairs(seed, first_pair, n_pairs, n_min, n_max, r_max, code, _ptr(verts), _ptr(off), _ptr(cnt), _ptr(prs))
+    return HullPool(verts, off, cnt, prs.reshape(-1, 2))
+
+
+def gjkepa_batch(pool: HullPool, version: int = 2, tol_ff: float = 1.0, precision: int = PREC_F64,
+                 device: int = 0) -> np.ndarray:
+    """Host-buffer batch on the GPU; returns a structured array of contact records."""
+    lib = load()
+    out = np.zeros(pool.n_pairs, dtype=record_dtype(precision))
+    verts = np.ascontiguousarray(pool.verts)
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    prs = np.ascontiguousarray(pool.pairs, np.int32).reshape(-1)
+    rc = lib.gjkepa_batch(int(version), float(tol_ff), pool.dtype_code, int(precision), _ptr(verts), verts.size,
+                          _ptr(off), _ptr(cnt), cnt.size, _ptr(prs), pool.n_pairs, _ptr(out), int(device))
+    _check(rc, "gjkepa_batch")
+    return out
+
+
+def workspace_bytes(n_pairs: int) -> int:
+    return int(load().gjkepa_workspace_bytes(n_pairs))
+
+
+def gjkepa_batch_device(version: int, tol_ff: float, vert_dtype: int, precision: int, verts_ptr: int,
+                        hull_off_ptr: int, hull_cnt_ptr: int, pairs_ptr: int, n_pairs: int, out_ptr: int,
+                        ws_ptr: int, ws_bytes: int, stream: int = 0) -> None:
+    """Device-resident batch (raw device pointers), asynchronous on `stream`."""
+    rc = load().gjkepa_batch_device(int(version), float(tol_ff), int(vert_dtype), int(precision), verts_ptr,
+                                    hull_off_ptr, hull_cnt_ptr, pairs_ptr, int(n_pairs), out_ptr, ws_ptr,
+                                    int(ws_bytes), stream or None)
+    _check(rc, "gjkepa_batch_device")
+
+
+def version_string() -> str:
+    return load().gjkepa_version_string().decode()

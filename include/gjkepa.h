@@ -1,0 +1,163 @@
+/*
+ * gjkepa.h — C-ABI drop-in boundary of the MI355X batched GJK/EPA narrow phase.
+ *
+ * The reference (xiejihong0306/collision-detect-GJK-EPA) exposes exactly one public entry,
+ * SUBROUTINE GJKEPA in MODULE GCLIB_GJKEPA (src/GCLIB_GJKEPA.f90:12, :39-52).  It answers one
+ * convex-pair query: hit flag, contact type, nearest points, normal, contact point and
+ * penetration depth.  The entries below are what an ISO_C_BINDING interface for that path binds:
+ *
+ *   gjkepa_query         one pair, same arguments / meaning as GJKEPA (GCLIB_GJKEPA.f90:39-52);
+ *                        host buffers, blocking.  The Fortran drop-in module
+ *                        (collision-detect-gjk-epa_amd/fortran/gclib_gjkepa.f90) wraps it
+ *                        under the unchanged GJKEPA signature.
+ *   gjkepa_batch         N pairs over a pooled hull set, host buffers, blocking.  This replaces
+ *                        the caller-side `!$OMP PARALLEL DO ... CALL GJKEPA` loop implied by the
+ *                        THREADPRIVATE design (GCLIB_GJKEPA.f90:9, :16, :55-60).
+ *   gjkepa_batch_device  the same with every buffer already resident in device memory (HBM),
+ *                        asynchronous on a caller stream; no allocation, no synchronisation,
+ *                        so it can be captured into a hipGraph.
+ *
+ * Error behaviour.  The reference has no return codes: it writes to unit 6 and then PAUSEs or
+ * STOPs (GCLIB_GJKEPA.f90:300-301, :337-339, :499-501, :635-637, :1370-1372).  Here every
+ * pair carries a status code instead (GJKEPA_STATUS_*), outputs are left at the values the
+ * reference would have returned (EPA cap: all zero with collision = 1, :299-302) or zeroed
+ * where the reference would have aborted, and the process never blocks.  Functions return
+ * 0 on success or a negative GJKEPA_E_* code.
+ *
+ * Data layout.  A hull is stored exactly like the reference's REAL*8 p(n,3) argument: column
+ * major, i.e. x[0..n-1], y[0..n-1], z[0..n-1] (structure of arrays per hull).  Hulls are pooled:
+ * hull h starts at scalar offset hull_off[h] of `verts` and has hull_cnt[h] vertices.  A pair
+ * is two hull indices (pairs[2k], pairs[2k+1]) = (p1_, p2_).
+ *
+ * Plain pointers and sizes only; no torch or HIP types in any signature.
+ */
+#ifndef GJKEPA_H
+#define GJKEPA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-pair status (replaces PAUSE / STOP) ---------------------------------------------- */
+#define GJKEPA_STATUS_OK          0  /* normal return */
+#define GJKEPA_STATUS_EPA_MAXITER 1  /* EPA hit its 99-iteration cap (:299-302): outputs 0, colli_type 0 */
+#define GJKEPA_STATUS_DEGENERATE  2  /* reference would STOP: degenerate plane (:1369-1373) etc. */
+#define GJKEPA_STATUS_BAD_VERSION 3  /* version_ not in {1,2,3} on a hit (:336-339) */
+#define GJKEPA_STATUS_BAD_INPUT   4  /* hull with < 1 vertex or above GJKEPA_MAX_HULL_VERTS */
+
+/* ---- API return codes ---------------------------------------------------------------------- */
+#define GJKEPA_E_OK          0
+#define GJKEPA_E_ARG        -1  /* invalid argument (null pointer, bad enum, bad size) */
+#define GJKEPA_E_HIP        -2  /* HIP runtime error (see gjkepa_last_error) */
+#define GJKEPA_E_NODEVICE   -3  /* no usable gfx950 device */
+#define GJKEPA_E_WORKSPACE  -4  /* device workspace too small */
+
+/* ---- enums --------------------------------------------------------------------------------- */
+#define GJKEPA_DTYPE_F32 0      /* vertex storage dtype */
+#define GJKEPA_DTYPE_F64 1
+#define GJKEPA_PREC_F64  1      /* compute precision: fp64 = the reference's REAL*8 semantics */
+#define GJKEPA_PREC_F32  0      /* compute precision: fp32 throughput path (tolerance-swept) */
+
+#define GJKEPA_MAX_HULL_VERTS 256   /* largest hull the kernels accept (config C4: 8..256) */
+
+/* ---- contact records (one per pair) ---------------------------------------------------------
+ * Field meaning follows GJKEPA's INTENT(OUT) arguments (GCLIB_GJKEPA.f90:47-52):
+ *   penetration_depth  <- penetration_depth_
+ *   collision_normal   <- collision_normal_(3)
+ *   collision_point    <- collision_point_(3)
+ *   nearest_points     <- nearest_points_(2,3), stored row-wise: p1 xyz then p2 xyz
+ *   collision          <- collision_ (LOGICAL*1)
+ *   colli_type         <- colliType_ (0 no hit / 1 other / 2 face-face)
+ *   status             <- GJKEPA_STATUS_*
+ *   diag               <- (gjk_iters) | (epa_iters << 8) | (final_faces << 16); diagnostics only
+ */
+typedef struct gjkepa_contact_f64 {
+    double   penetration_depth;
+    double   collision_normal[3];
+    double   collision_point[3];
+    double   nearest_points[6];
+    int8_t   collision;
+    int8_t   colli_type;
+    int8_t   status;
+    int8_t   reserved;
+    uint32_t diag;
+    uint32_t pad[4];
+} gjkepa_contact_f64;            /* 128 bytes */
+
+typedef struct gjkepa_contact_f32 {
+    float    penetration_depth;
+    float    collision_normal[3];
+    float    collision_point[3];
+    float    nearest_points[6];
+    int8_t   collision;
+    int8_t   colli_type;
+    int8_t   status;
+    int8_t   reserved;
+    uint32_t diag;
+    uint32_t pad;
+} gjkepa_contact_f32;            /* 64 bytes */
+
+/* Size in bytes of one contact record for a compute precision (128 for F64, 64 for F32). */
+int gjkepa_record_bytes(int32_t precision);
+
+/* ---- single pair: the GJKEPA drop-in (GCLIB_GJKEPA.f90:39-52) ---------------------------------
+ * p1, p2: REAL*8 (n,3) column-major, exactly the memory of the Fortran assumed-shape actuals.
+ * nearest_points: REAL*8 (2,3) column-major (Fortran layout: p1x p2x p1y p2y p1z p2z).
+ * status may be NULL.  Runs on device `device` (batch of one); blocking; thread-safe. */
+int gjkepa_query(int32_t version, double tol_ff,
+                 const double* p1, int32_t n1,
+                 const double* p2, int32_t n2,
+                 int8_t* collision, int32_t* colli_type,
+                 double* nearest_points, double* collision_normal,
+                 double* collision_point, double* penetration_depth,
+                 int32_t* status, int32_t device);
+
+/* ---- batch over host buffers (blocking) ------------------------------------------------------
+ * verts:     hull vertex pool, dtype `vert_dtype`, n_vert_scalars scalars in total.
+ * hull_off:  [n_hulls] scalar offset of each hull's x[0] in `verts`.
+ * hull_cnt:  [n_hulls] vertex count of each hull (1..GJKEPA_MAX_HULL_VERTS).
+ * pairs:     [2*n_pairs] hull indices (p1_, p2_) per pair.
+ * out:       [n_pairs] records, gjkepa_contact_f64 (precision F64) or _f32 (precision F32). */
+int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                 const void* verts, int64_t n_vert_scalars,
+                 const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
+                 const int32_t* pairs, int64_t n_pairs,
+                 void* out, int32_t device);
+
+/* ---- batch over device buffers (asynchronous on `stream`, a hipStream_t or NULL) -------------
+ * All pointers are device pointers on the current device.  `workspace` must hold at least
+ * gjkepa_workspace_bytes(n_pairs) bytes; it is scratch for the large-polytope overflow pass
+ * and may be reused between calls on the same stream. */
+int64_t gjkepa_workspace_bytes(int64_t n_pairs);
+int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                        const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                        const int32_t* pairs, int64_t n_pairs,
+                        void* out, void* workspace, int64_t workspace_bytes,
+                        void* stream);
+
+/* Last error message of the calling thread ("" if none). */
+const char* gjkepa_last_error(void);
+
+/* Library build string (kernels' target, caps, compile flags). */
+const char* gjkepa_version_string(void);
+
+/* ---- synthetic workload generator (deterministic, counter-based SplitMix64) ----
+ * Fills a hull pool for `n_pairs` pairs with two private hulls per pair (hull 2k = p1_, 2k+1 = p2_):
+ * vertices are unit vectors about the hull centre (all extreme), hull A centred at 0, hull B at
+ * u*r with u uniform on S^2 and r ~ U[0, r_max].  Hull sizes are n_min..n_max (uniform integer;
+ * n_min == n_max for fixed-size configs).  Values are rounded to fp32 so the fp32 and fp64 pools
+ * hold identical numbers.  `first_pair` offsets the counter so shards of one logical job agree.
+ * hull_off/hull_cnt/pairs are written for the generated pool (pairs are global hull indices of
+ * this pool, i.e. 2k, 2k+1).  Pass verts == NULL to only compute sizes: returns the number of
+ * vertex scalars the pool needs. */
+int64_t gjkepa_synth_pairs(uint64_t seed, int64_t first_pair, int64_t n_pairs,
+                           int32_t n_min, int32_t n_max, double r_max,
+                           int32_t vert_dtype, void* verts,
+                           int64_t* hull_off, int32_t* hull_cnt, int32_t* pairs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GJKEPA_H */

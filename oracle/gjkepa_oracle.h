@@ -1,0 +1,41 @@
+/*
+ * gjkepa_oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference GJK/EPA path
+ * (src/GCLIB_GJKEPA.f90 of xiejihong0306/collision-detect-GJK-EPA), used by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.  The product
+ * (libgjkepa_hip.so and the Fortran drop-in) never links or calls this code.
+ *
+ * PARITY UNPINNED against the reference's own outputs: the reference ships no tests or golden
+ * vectors, and it cannot be built here (it USEs the unvendored GCLIB_List / GCLIB_QuickHull /
+ * GCLIB_DeHull modules, GCLIB_GJKEPA.f90:13-15, and ifort-only extensions).  The restatement is
+ * cross-checked instead against (a) the known-answer cube cases recorded in SURVEY.md
+ * Appendix C and (b) independent geometric ground truth (scipy Qhull of the Minkowski difference).
+ * See DESIGN.md §Oracle.
+ */
+#ifndef GJKEPA_ORACLE_H
+#define GJKEPA_ORACLE_H
+#include <stdint.h>
+#include "../include/gjkepa.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One pair, fp64.  p1/p2 column-major (n,3).  Fills a gjkepa_contact_f64 record. */
+int oracle_gjkepa(int32_t version, double tol_ff,
+                  const double* p1, int32_t n1, const double* p2, int32_t n2,
+                  gjkepa_contact_f64* out);
+
+/* Batch over a hull pool (same layout as gjkepa_batch); OpenMP over pairs with `nthreads`
+ * threads (<= 0: OpenMP default).  vert_dtype F32 pools are upcast to fp64. */
+int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
+                        const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                        const int32_t* pairs, int64_t n_pairs,
+                        gjkepa_contact_f64* out, int32_t nthreads);
+
+/* Number of OpenMP threads the batch call would use for nthreads <= 0. */
+int oracle_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU restatement (oracle/gjkepa_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this, and only as the
+checker / CPU baseline.  Parity with the reference is unpinned (see gjkepa_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libgjkepa_oracle.so")
+
+REC64 = np.dtype([
+    ("penetration_depth", "<f8"), ("collision_normal", "<f8", (3,)), ("collision_point", "<f8", (3,)),
+    ("nearest_points", "<f8", (6,)), ("collision", "i1"), ("colli_type", "i1"), ("status", "i1"),
+    ("reserved", "i1"), ("diag", "<u4"), ("pad", "<u4", (4,)),
+])
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        lib.oracle_gjkepa.argtypes = [i32, dbl, vp, i32, vp, i32, vp]
+        lib.oracle_gjkepa.restype = ctypes.c_int
+        lib.oracle_gjkepa_batch.argtypes = [i32, dbl, i32, vp, vp, vp, vp, i64, vp, i32]
+        lib.oracle_gjkepa_batch.restype = ctypes.c_int
+        lib.oracle_max_threads.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def gjkepa(version: int, tol_ff: float, p1, p2) -> np.ndarray:
+    """One pair; p1, p2 are (n, 3).  Returns a REC64 record (0-d structured array)."""
+    a = np.ascontiguousarray(np.asarray(p1, np.float64).T)
+    b = np.ascontiguousarray(np.asarray(p2, np.float64).T)
+    out = np.zeros(1, REC64)
+    rc = load().oracle_gjkepa(int(version), float(tol_ff), a.ctypes.data, a.shape[1], b.ctypes.data, b.shape[1],
+                              out.ctypes.data)
+    assert rc == 0
+    return out[0]
+
+
+def gjkepa_batch(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0) -> np.ndarray:
+    """Batch over a gjkepa.HullPool-like object (verts, hull_off, hull_cnt, pairs)."""
+    verts = np.ascontiguousarray(pool.verts)
+    code = 0 if verts.dtype == np.float32 else 1
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    prs = np.ascontiguousarray(pool.pairs, np.int32).reshape(-1)
+    n = prs.size // 2
+    out = np.zeros(n, REC64)
+    rc = load().oracle_gjkepa_batch(int(version), float(tol_ff), code, verts.ctypes.data, off.ctypes.data,
+                                    cnt.ctypes.data, prs.ctypes.data, n, out.ctypes.data, int(nthreads))
+    assert rc == 0
+    return out
+
+
+def max_threads() -> int:
+    return int(load().oracle_max_threads())
