@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: M convex-pair GJK+EPA queries/s on N x MI355X (BASELINE.json metric).
+
+Workload (N=1) = BASELINE config C2: 2^20 random 32-vertex convex-hull pairs, fp32 vertex storage,
+version_=2, TOL_FF_=1.0, hull B centre offset r ~ U[0, 2.5] (seed 0x6A4B5C1D).
+A "step" is one pass of the hot path (gjkepa_batch_device: the tiered GJK/EPA kernels) over the
+whole batch, with hulls, pair list and output already resident in HBM.  For N > 1 each rank owns
+a contiguous shard of `--pairs-per-gpu` pairs (weak scaling) and every step ends with an RCCL
+all-gather of the contact records over xGMI (config C3's exchange).
+
+Extra legs (not timed in `value`): the roofline of the dominant kernel from HIP events on the
+launch stream, and on rank 0 at N=1 a CPU baseline — the oracle restatement (kind "port") over a
+bounded sample of the same pairs, which also re-checks GPU/CPU parity on that sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "collision-detect-gjk-epa_amd"))
+
+import numpy as np  # noqa: E402
+
+import gjkepa  # noqa: E402
+
+SEED = 0x6A4B5C1D
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "M convex-pair GJK+EPA queries/sec at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def algorithmic_bytes_per_query(n1: int, n2: int, vert_bytes: int, rec_bytes: int) -> int:
+    """Bytes one query must move through HBM: both hulls' vertices (SoA), the pair's two hull
+    indices, the two hulls' (offset, count) and the contact record it writes."""
+    return vert_bytes * 3 * (n1 + n2) + 2 * 4 + 2 * (8 + 4) + rec_bytes
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--nverts", type=int, default=32)
+    ap.add_argument("--rmax", type=float, default=2.5)
+    ap.add_argument("--version", type=int, default=2)
+    ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather for N>1")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 18)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    lib = gjkepa.load()
+
+    n = args.pairs_per_gpu
+    prec = gjkepa.PREC_F64 if args.precision == "f64" else gjkepa.PREC_F32
+    rec_bytes = lib.gjkepa_record_bytes(prec)
+    pool = gjkepa.synth_pairs(SEED, n, args.nverts, args.nverts, args.rmax, first_pair=rank * n, dtype=np.float32)
+    verts = torch.from_numpy(pool.verts).to(dev)
+    off = torch.from_numpy(pool.hull_off).to(dev)
+    cnt = torch.from_numpy(pool.hull_cnt).to(dev)
+    prs = torch.from_numpy(pool.pairs.reshape(-1)).to(dev)
+    out = torch.zeros(n * rec_bytes, dtype=torch.uint8, device=dev)
+    ws_bytes = gjkepa.workspace_bytes(n)
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+    gathered = None
+    if world > 1 and not args.no_gather:
+        gathered = torch.empty(world * n * rec_bytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def launch(p):
+        gjkepa.gjkepa_batch_device(args.version, 1.0, gjkepa.DTYPE_F32, p, verts.data_ptr(), off.data_ptr(),
+                                   cnt.data_ptr(), prs.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes, sptr)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        launch(prec)
+        if i is not None:
+            ev[i][1].record(stream)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    ms_per_step = 1e3 * elapsed / args.steps
+    total_pairs = n * world
+    value = total_pairs * args.steps / elapsed / 1e6
+
+    # statistics of the last step's records (rank-local)
+    recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
+    hit_rate = float((recs["collision"] != 0).mean())
+    status_counts = {int(k): int(v) for k, v in zip(*np.unique(recs["status"], return_counts=True))}
+    epa_iters = (recs["diag"] >> 8) & 0xFF
+    epa_mean = float(epa_iters[recs["collision"] != 0].mean()) if hit_rate > 0 else 0.0
+
+    bpq = algorithmic_bytes_per_query(args.nverts, args.nverts, 4, rec_bytes)
+    achieved = n * bpq / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            pj = json.load(open(prof))
+            key = f"{args.precision}_{args.nverts}_{n}"
+            if key in pj:
+                traffic = pj[key]["bytes_per_launch"]
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic,
+                "bytes_per_query": bpq, "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
+                "kernel": "gjkepa_tier_kernel (tiers 0-2 + memset, HIP events on the launch stream)"}
+
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "M queries/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.precision, "data": "synthetic",
+        "config": {"workload": f"C2: random {args.nverts}-vertex convex-hull pairs, fp32 vertex storage, "
+                               f"{args.precision} compute, version_={args.version}, TOL_FF_=1.0, r~U[0,{args.rmax}]",
+                   "pairs_per_gpu": n, "total_pairs": total_pairs, "seed": SEED,
+                   "parallelism": f"shard{world}" + ("+allgather" if gathered is not None else ""),
+                   "vert_storage": "f32", "record_bytes": rec_bytes},
+        "roofline": roofline,
+        "hit_rate": round(hit_rate, 4), "epa_iters_mean": round(epa_mean, 2), "status_counts": status_counts,
+        "lib": gjkepa.version_string(),
+    }
+
+    # fp32-compute side measurement (same batch), reported, never `value`
+    if rank == 0 and world == 1 and not args.no_f32_leg and prec == gjkepa.PREC_F64:
+        out32 = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+        def l32():
+            gjkepa.gjkepa_batch_device(args.version, 1.0, gjkepa.DTYPE_F32, gjkepa.PREC_F32, verts.data_ptr(),
+                                       off.data_ptr(), cnt.data_ptr(), prs.data_ptr(), n, out32.data_ptr(),
+                                       ws.data_ptr(), ws_bytes, sptr)
+        l32()
+        torch.cuda.synchronize(dev)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(args.steps):
+            l32()
+        e.record(stream)
+        torch.cuda.synchronize(dev)
+        ms32 = s.elapsed_time(e) / args.steps
+        r32 = np.frombuffer(out32.cpu().numpy().tobytes(), dtype=gjkepa.REC32)
+        result["fp32_compute"] = {"value": round(n / (ms32 * 1e-3) / 1e6, 3), "unit": "M queries/s",
+                                  "hit_agreement_vs_f64": round(float((r32["collision"] == recs["collision"]).mean()), 6)}
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker / CPU baseline only
+        m = min(args.cpu_sample, n)
+        sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:m])
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+        oracle.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:256]),
+                            args.version, 1.0, threads)
+        t = time.perf_counter()
+        cref = oracle.gjkepa_batch(sub, args.version, 1.0, threads)
+        ct = time.perf_counter() - t
+        result["cpu_baseline"] = {
+            "value": round(m / ct / 1e6, 4), "unit": "M queries/s", "cores": threads, "kind": "port",
+            "sample": f"first {m} pairs of the same C2 batch, fp64 oracle restatement (oracle/gjkepa_oracle.c), "
+                      f"OpenMP dynamic over pairs, {ct:.2f} s wall",
+        }
+        if prec == gjkepa.PREC_F64:
+            g = recs[:m]
+            same = (g.tobytes() == cref.tobytes())
+            eq = np.frombuffer(g.tobytes(), np.uint8).reshape(m, -1) == np.frombuffer(cref.tobytes(), np.uint8).reshape(m, -1)
+            result["parity_sample"] = {"pairs": m, "bitexact_records": float(eq.all(axis=1).mean()), "all_equal": bool(same)}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -326,6 +326,8 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
                double* depth, v3* normal, int* iters) {
     static const int SOUP[4][3] = {{0, 1, 2}, {0, 2, 3}, {0, 1, 3}, {1, 2, 3}};   /* :279-293 */
     int iter = 0;
+    H->nv = 0;
+    H->nf = 0;
     for (;;) {
         ++iter;
         *iters = iter;
@@ -664,7 +666,7 @@ static int gjkepa_pair(int32_t version, double tol_ff, const hull_t* A, const hu
             if (norm2(cross(vsub(S[1], S[0]), vsub(S[2], S[1]))) < TOL_PT) return 0;   /* :199-201 */
             double r;
             st = dist_pf_sign(S[3], S[0], S[1], S[2], &r);                     /* :203 */
-            if (st) goto fail;
+            if (st) { out->diag = (uint32_t)(gjk_it & 0xff); goto fail; }
             if (fabs(r) < TOL_PT) return 0;
             if (is_point_in_simplex(ORIGIN, S)) { hit = 1; break; }            /* :210-216 */
             int over = 1;                                                      /* :219-234 */

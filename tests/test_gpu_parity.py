@@ -1,0 +1,169 @@
+"""GPU parity tests (MI355X): the HIP path through the C-ABI against the oracle.
+
+Bar (north_star): hit flag bit-exact, penetration depth / normal within 1e-6 relative.  The fp64
+path is held to more: every contact record must be byte-identical to the oracle's (same arithmetic
+recipe, no FMA contraction).  The fp32-compute throughput path is held to the tolerance recorded in
+test_fp32_tolerance_sweep.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import gjkepa
+import parity
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CUBE = np.array([[x, y, z] for z in (0, 1) for y in (0, 1) for x in (0, 1)], float)
+RTOL = 1e-6   # north_star: within 1e-6 relative on penetration depth and normal
+
+
+def _bytes(a):
+    return a.view(np.uint8).reshape(len(a), -1)
+
+
+def assert_bitexact(g, r, what=""):
+    c = parity.compare(g, r, rtol=RTOL)
+    assert c["ok"], (what, {k: c[k] for k in c if k != "bad_idx"}, [parity.fmt(g[i]) + " | " + parity.fmt(r[i]) for i in c["bad_idx"][:3]])
+    same = (_bytes(g) == _bytes(r)).all(axis=1)
+    assert same.all(), (what, "records differ bytewise", np.nonzero(~same)[0][:10])
+
+
+@pytest.mark.parametrize("name", ["c1_cubes", "c2_32v", "c4_mixed", "c5_deep"])
+@pytest.mark.parametrize("version", [1, 2, 3])
+def test_golden_fixtures_on_gpu(name, version):
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    pool = gjkepa.HullPool(z["verts"], z["hull_off"], z["hull_cnt"], z["pairs"])
+    g = gjkepa.gjkepa_batch(pool, version, float(z["tol_ff"]))
+    ref = z[f"rec_v{version}"].reshape(-1).view(gjkepa.REC64)
+    assert_bitexact(g, ref, f"{name} v{version}")
+
+
+@pytest.mark.parametrize("off", [(0.5, 0.2, 0.1), (1, 0, 0), (0, 0, 1e-3), (0.5, 0.5, 0.1), (3, 0, 0), (0, 0, 0)])
+@pytest.mark.parametrize("version", [1, 2, 3])
+def test_single_query_api_matches_oracle(orc, off, version):
+    b = CUBE + np.asarray(off, float)
+    c = gjkepa.gjkepa(version, 1e-3, CUBE, b)
+    r = orc.gjkepa(version, 1e-3, CUBE, b)
+    assert c.collision == bool(r["collision"]) and c.colli_type == r["colli_type"] and c.status == r["status"]
+    for got, want in [(c.penetration_depth, r["penetration_depth"]), (c.collision_normal, r["collision_normal"]),
+                      (c.collision_point, r["collision_point"]), (c.nearest_points.reshape(-1), r["nearest_points"])]:
+        np.testing.assert_array_equal(np.asarray(got), np.asarray(want))
+
+
+def test_c1_config_known_answer():
+    c = gjkepa.gjkepa(2, 1.0, CUBE, CUBE + np.array([0.5, 0.2, 0.1]))
+    assert c.collision and c.colli_type == 2 and c.status == 0
+    assert c.penetration_depth == pytest.approx(0.5, abs=1e-14)
+    assert np.allclose(c.collision_normal, [1, 0, 0]) and np.allclose(c.collision_point, [1, 0.5, 0.5])
+
+
+@pytest.mark.parametrize("cfg", [("C2", 32, 32, 2.5, 20000), ("C4", 8, 256, 2.5, 3000), ("C5", 32, 128, 0.3, 3000),
+                                 ("shallow", 16, 48, 2.2, 4000)])
+def test_seeded_sets_bitexact(orc, cfg):
+    name, lo, hi, rmax, n = cfg
+    pool = gjkepa.synth_pairs(0xBEEF + n, n, lo, hi, rmax)
+    for v in (2, 1):
+        assert_bitexact(gjkepa.gjkepa_batch(pool, v, 1.0), orc.gjkepa_batch(pool, v, 1.0), f"{name} v{v}")
+
+
+def test_fp64_vertex_storage(orc):
+    pool = gjkepa.synth_pairs(99, 2000, 8, 80, 2.0, dtype=np.float64)
+    rng = np.random.default_rng(5)
+    pool.verts += rng.normal(scale=1e-7, size=pool.verts.shape)      # not fp32-representable
+    assert_bitexact(gjkepa.gjkepa_batch(pool, 2, 1.0), orc.gjkepa_batch(pool, 2, 1.0), "fp64 storage")
+
+
+def _edge_pool():
+    rng = np.random.default_rng(11)
+    sq = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]], float)
+    big = rng.normal(size=(256, 3))
+    big /= np.linalg.norm(big, axis=1, keepdims=True)
+    pairs = [
+        (CUBE, CUBE),                                       # identical hulls: reference aborts
+        (CUBE, CUBE + [1e-13, 0, 0]),
+        (np.zeros((1, 3)), CUBE - 0.5),                     # single point inside a cube
+        (np.zeros((1, 3)) + 5, CUBE),                       # single point far away
+        (np.zeros((1, 3)), np.zeros((1, 3))),               # point vs same point
+        (sq, sq + [0.2, 0.3, 0]),                           # coplanar (flat) hulls
+        (sq, sq + [0.2, 0.3, 0.5]),
+        (np.vstack([CUBE, CUBE]), CUBE + 0.25),             # duplicated vertices
+        (big, big * 0.5 + 0.3),                             # maximum hull size
+        (big, big + [1.9, 0, 0]),
+        (big[:65], big[:200] + 0.1),                        # just above tier-0 capacity
+        (CUBE * 1e-3, CUBE * 1e-3 + 2e-4),                  # small scale: absolute tolerances bite
+        (CUBE * 1e3, CUBE * 1e3 + [500, 200, 100]),         # large scale
+        (CUBE, CUBE + [1 - 1e-9, 0, 0]),                    # barely touching
+    ]
+    return gjkepa.HullPool.from_pairs(pairs, dtype=np.float64)
+
+
+@pytest.mark.parametrize("version", [1, 2, 3])
+def test_edge_cases(orc, version):
+    pool = _edge_pool()
+    assert_bitexact(gjkepa.gjkepa_batch(pool, version, 1.0), orc.gjkepa_batch(pool, version, 1.0), f"edge v{version}")
+
+
+def test_bad_inputs_status():
+    pool = gjkepa.HullPool.from_pairs([(CUBE, CUBE + [0.5, 0.2, 0.1]), (np.zeros((0, 3)), CUBE), (np.ones((257, 3)), CUBE)])
+    nan = pool.verts.copy()
+    g = gjkepa.gjkepa_batch(pool, 2, 1.0)
+    assert g["status"].tolist() == [0, gjkepa.STATUS_BAD_INPUT, gjkepa.STATUS_BAD_INPUT]
+    nan[0] = np.nan
+    g = gjkepa.gjkepa_batch(gjkepa.HullPool(nan, pool.hull_off, pool.hull_cnt, pool.pairs), 2, 1.0)
+    assert g["status"][0] == gjkepa.STATUS_BAD_INPUT
+
+
+def test_bad_version_status(orc):
+    pool = gjkepa.HullPool.from_pairs([(CUBE, CUBE + [0.5, 0.2, 0.1]), (CUBE, CUBE + 3)])
+    g = gjkepa.gjkepa_batch(pool, 4, 1.0)
+    assert g["status"].tolist() == [gjkepa.STATUS_BAD_VERSION, 0]
+    assert_bitexact(g, orc.gjkepa_batch(pool, 4, 1.0), "bad version")
+
+
+def test_empty_batch():
+    pool = gjkepa.HullPool(np.zeros(0, np.float32), np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros((0, 2), np.int32))
+    assert len(gjkepa.gjkepa_batch(pool)) == 0
+
+
+def test_pooled_hulls_shared_between_pairs(orc):
+    # one hull pool, many pairs referencing the same hulls (broad-phase style pair list)
+    base = gjkepa.synth_pairs(3, 64, 12, 40, 1.5)
+    rng = np.random.default_rng(0)
+    prs = rng.integers(0, 128, size=(5000, 2)).astype(np.int32)
+    pool = gjkepa.HullPool(base.verts, base.hull_off, base.hull_cnt, prs)
+    assert_bitexact(gjkepa.gjkepa_batch(pool, 2, 1.0), orc.gjkepa_batch(pool, 2, 1.0), "pooled")
+
+
+def test_device_api_matches_host_api():
+    import torch
+
+    pool = gjkepa.synth_pairs(17, 50000, 32, 32, 2.5)
+    host = gjkepa.gjkepa_batch(pool, 2, 1.0)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+         dict(v=pool.verts, o=pool.hull_off, c=pool.hull_cnt, p=pool.pairs.reshape(-1)).items()}
+    out = torch.zeros(pool.n_pairs * 128, dtype=torch.uint8, device=dev)
+    wsb = gjkepa.workspace_bytes(pool.n_pairs)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        gjkepa.gjkepa_batch_device(2, 1.0, gjkepa.DTYPE_F32, gjkepa.PREC_F64, t["v"].data_ptr(), t["o"].data_ptr(),
+                                   t["c"].data_ptr(), t["p"].data_ptr(), pool.n_pairs, out.data_ptr(), ws.data_ptr(),
+                                   wsb, s.cuda_stream)
+    s.synchronize()
+    assert out.cpu().numpy().tobytes() == host.tobytes()
+
+
+def test_fp32_tolerance_sweep(orc):
+    """fp32 compute (throughput path): hit flags vs the fp64 oracle, depth/normal error bounds."""
+    for name, lo, hi, rmax in [("C2", 32, 32, 2.5), ("C5", 64, 128, 0.3)]:
+        pool = gjkepa.synth_pairs(0x6A4B5C1D, 4000, lo, hi, rmax)
+        g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F32)
+        r = orc.gjkepa_batch(pool, 2, 1.0)
+        agree = (g["collision"] == r["collision"]).mean()
+        assert agree >= 0.999, (name, agree)
+        m = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
+        d = np.abs(g["penetration_depth"][m] - r["penetration_depth"][m])
+        assert np.quantile(d, 0.99) < 1e-4 and d.max() < 5e-3, (name, np.quantile(d, 0.99), d.max())
