@@ -80,9 +80,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     if (n_pairs == 0) return 0;
     if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
     char* ws = (char*)workspace;
-    int32_t* counts = (int32_t*)ws;                      // [0] tier-1 list size, [1] tier-2 list size
-    int32_t* list1 = (int32_t*)(ws + kWsHeader);
-    int32_t* list2 = list1 + n_pairs;
+    int32_t* counts = (int32_t*)ws;                      // [t-1]: size of tier t's work list
     hipError_t e = hipMemsetAsync(counts, 0, kWsHeader, s);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     gjkepa_tier_args a{};
@@ -96,18 +94,16 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.out = out;
     a.num_cus = num_cus;
     a.grid = 0;
-    // tier 0: every pair
-    a.in_list = nullptr; a.in_count = nullptr; a.out_list = list1; a.out_count = counts + 0;
-    e = gjkepa_launch_tier(0, vert_dtype, precision, a, s);
-    if (e != hipSuccess) return hip_fail(e, "tier 0 launch");
-    // tier 1: pairs deferred by tier 0
-    a.in_list = list1; a.in_count = counts + 0; a.out_list = list2; a.out_count = counts + 1;
-    e = gjkepa_launch_tier(1, vert_dtype, precision, a, s);
-    if (e != hipSuccess) return hip_fail(e, "tier 1 launch");
-    // tier 2: worst-case capacities, never defers
-    a.in_list = list2; a.in_count = counts + 1; a.out_list = nullptr; a.out_count = nullptr;
-    e = gjkepa_launch_tier(2, vert_dtype, precision, a, s);
-    if (e != hipSuccess) return hip_fail(e, "tier 2 launch");
+    for (int t = 0; t < GJKEPA_NUM_TIERS; ++t) {
+        // tier 0 takes every pair; tier t > 0 the pairs tier t-1 deferred; the last never defers
+        a.in_list = t == 0 ? nullptr : (const int32_t*)(ws + kWsHeader) + (int64_t)(t - 1) * n_pairs;
+        a.in_count = t == 0 ? nullptr : counts + (t - 1);
+        const bool last = t == GJKEPA_NUM_TIERS - 1;
+        a.out_list = last ? nullptr : (int32_t*)(ws + kWsHeader) + (int64_t)t * n_pairs;
+        a.out_count = last ? nullptr : counts + t;
+        e = gjkepa_launch_tier(t, vert_dtype, precision, a, s);
+        if (e != hipSuccess) return hip_fail(e, "tier launch");
+    }
     return 0;
 }
 
@@ -128,7 +124,7 @@ int gjkepa_record_bytes(int32_t precision) {
 
 int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
     if (n_pairs < 0) return GJKEPA_E_ARG;
-    return kWsHeader + 2 * (int64_t)sizeof(int32_t) * n_pairs;
+    return kWsHeader + (GJKEPA_NUM_TIERS - 1) * (int64_t)sizeof(int32_t) * n_pairs;
 }
 
 const char* gjkepa_last_error(void) { return g_err.c_str(); }
@@ -136,10 +132,11 @@ const char* gjkepa_last_error(void) { return g_err.c_str(); }
 const char* gjkepa_version_string(void) {
     static char buf[256];
     std::snprintf(buf, sizeof(buf),
-                  "gjkepa-mi355x gfx950 wave64; tiers K/VCAP/FCAP = %d/%d/%d, %d/%d/%d, %d/%d/%d; "
-                  "-O3 -ffp-contract=off",
-                  GJKEPA_T0_K, GJKEPA_T0_VCAP, GJKEPA_T0_FCAP, GJKEPA_T1_K, GJKEPA_T1_VCAP, GJKEPA_T1_FCAP,
-                  GJKEPA_T2_K, GJKEPA_T2_VCAP, GJKEPA_T2_FCAP);
+                  "gjkepa-mi355x gfx950 wave64; tiers G/K/VCAP/FCAP = %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, "
+                  "%d/%d/%d/%d; -O3 -ffp-contract=off",
+                  GJKEPA_T0_G, GJKEPA_T0_K, GJKEPA_T0_VCAP, GJKEPA_T0_FCAP, GJKEPA_T1_G, GJKEPA_T1_K, GJKEPA_T1_VCAP,
+                  GJKEPA_T1_FCAP, GJKEPA_T2_G, GJKEPA_T2_K, GJKEPA_T2_VCAP, GJKEPA_T2_FCAP, GJKEPA_T3_G, GJKEPA_T3_K,
+                  GJKEPA_T3_VCAP, GJKEPA_T3_FCAP);
     return buf;
 }
 

@@ -1,8 +1,8 @@
 // gjkepa_kernel.h — host-side interface of the tiered GJK/EPA kernels (internal, not the C-ABI).
 //
-// Tiers: every pair first runs in tier 0 (hulls up to 64*T0_K vertices, EPA polytope up to
-// T0_VCAP vertices / T0_FCAP faces).  A pair that does not fit is appended, on the device, to
-// tier 1's work list, and so on; tier 2 holds the worst case the reference allows
+// Tiers: every pair first runs in tier 0 (hulls up to G*K vertices, EPA polytope up to
+// VCAP vertices / FCAP faces).  A pair that does not fit is appended, on the device, to the next
+// tier's work list, and so on; the last tier holds the worst case the reference allows
 // (6 + 2*99 EPA points, 2*V-4 faces), so it never defers.  Deferral recomputes the pair from
 // scratch, so results do not depend on which tier produced them.
 #pragma once
@@ -11,16 +11,25 @@
 #include <cstddef>
 #include <cstdint>
 
-#define GJKEPA_T0_K 1
-#define GJKEPA_T0_VCAP 64
-#define GJKEPA_T0_FCAP 128
-#define GJKEPA_T1_K 4
-#define GJKEPA_T1_VCAP 96
-#define GJKEPA_T1_FCAP 192
+// tier t: G lanes per pair (64/G pairs per wave), K vertices per lane per hull (hull <= G*K),
+// EPA polytope capacity VCAP vertices / FCAP faces
+#define GJKEPA_T0_G 16
+#define GJKEPA_T0_K 2
+#define GJKEPA_T0_VCAP 40
+#define GJKEPA_T0_FCAP 64
+#define GJKEPA_T1_G 64
+#define GJKEPA_T1_K 1
+#define GJKEPA_T1_VCAP 64
+#define GJKEPA_T1_FCAP 128
+#define GJKEPA_T2_G 64
 #define GJKEPA_T2_K 4
-#define GJKEPA_T2_VCAP 208
-#define GJKEPA_T2_FCAP 416
-#define GJKEPA_NUM_TIERS 3
+#define GJKEPA_T2_VCAP 104
+#define GJKEPA_T2_FCAP 208
+#define GJKEPA_T3_G 64
+#define GJKEPA_T3_K 4
+#define GJKEPA_T3_VCAP 208
+#define GJKEPA_T3_FCAP 416
+#define GJKEPA_NUM_TIERS 4
 
 struct gjkepa_tier_args {
     int version;
@@ -40,4 +49,3 @@ struct gjkepa_tier_args {
 };
 
 hipError_t gjkepa_launch_tier(int tier, int vert_dtype, int precision, const gjkepa_tier_args& a, hipStream_t s);
-size_t gjkepa_tier_lds_bytes(int tier, int precision);
