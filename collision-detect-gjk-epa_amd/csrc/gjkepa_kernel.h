@@ -13,22 +13,54 @@
 
 // tier t: G lanes per pair (64/G pairs per wave), K vertices per lane per hull (hull <= G*K),
 // EPA polytope capacity VCAP vertices / FCAP faces
+#ifndef GJKEPA_T0_G
 #define GJKEPA_T0_G 16
+#endif
+#ifndef GJKEPA_T0_K
 #define GJKEPA_T0_K 2
+#endif
+#ifndef GJKEPA_T0_VCAP
 #define GJKEPA_T0_VCAP 40
+#endif
+#ifndef GJKEPA_T0_FCAP
 #define GJKEPA_T0_FCAP 64
+#endif
+#ifndef GJKEPA_T1_G
 #define GJKEPA_T1_G 64
+#endif
+#ifndef GJKEPA_T1_K
 #define GJKEPA_T1_K 1
+#endif
+#ifndef GJKEPA_T1_VCAP
 #define GJKEPA_T1_VCAP 64
+#endif
+#ifndef GJKEPA_T1_FCAP
 #define GJKEPA_T1_FCAP 128
+#endif
+#ifndef GJKEPA_T2_G
 #define GJKEPA_T2_G 64
+#endif
+#ifndef GJKEPA_T2_K
 #define GJKEPA_T2_K 4
+#endif
+#ifndef GJKEPA_T2_VCAP
 #define GJKEPA_T2_VCAP 104
+#endif
+#ifndef GJKEPA_T2_FCAP
 #define GJKEPA_T2_FCAP 208
+#endif
+#ifndef GJKEPA_T3_G
 #define GJKEPA_T3_G 64
+#endif
+#ifndef GJKEPA_T3_K
 #define GJKEPA_T3_K 4
+#endif
+#ifndef GJKEPA_T3_VCAP
 #define GJKEPA_T3_VCAP 208
+#endif
+#ifndef GJKEPA_T3_FCAP
 #define GJKEPA_T3_FCAP 416
+#endif
 #define GJKEPA_NUM_TIERS 4
 
 struct gjkepa_tier_args {

@@ -320,7 +320,9 @@ CTX_T DEV void write_face(CTX& c, int f, int a, int b, int d, V3<T> n, T dist) {
 
 // Add point p (vertex id k; appended at nv when `append`) — visible faces (signed distance >
 // HULL) removed, horizon coned to k.  Order: survivors, then new faces by (visible face, edge).
-CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexist) {
+// `changed` reports whether the hull changed; with `save_eq` the current distances are copied to
+// dsv[] when the face count will not change (the only case the termination test reads them).
+CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexist, bool& changed, bool save_eq) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
@@ -338,6 +340,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         nvis += popc(vm[r]);
     }
     nvis = c.g.uni(nvis);
+    changed = nvis > 0;
     if (nvis == 0) return 0;
     int k = kexist;
     if (append) {
@@ -386,10 +389,21 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
     nh = c.g.uni(nh);
     const int nf2 = nf - nvis + nh;
     if (nh > FC || nf2 > FC) return ST_DEFER;
-    // compact surviving faces (order preserved; in place is safe: new index <= old index)
+    if (save_eq && nf2 == nf) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int f = r * G + gl;
+            if (f < nf) E.dsv[f] = E.fd[f];
+        }
+    }
+    // compact surviving faces (order preserved; in place is safe: new index <= old index).
+    // Rows before the first visible face do not move.
     int base = 0;
+    bool moving = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        moving = moving || vm[r] != 0;
+        if (!moving) { base += G; continue; }
         int f = r * G + gl;
         bool keep = f < nf && !c.g.bit(vm[r]);
         uint32_t fv = 0;
@@ -399,7 +413,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         __builtin_amdgcn_wave_barrier();
         if (keep) {
             int pos = base + mbcnt(m);
-            E.fv[pos] = fv; E.fnx[pos] = nx; E.fny[pos] = ny; E.fnz[pos] = nz; E.fd[pos] = d;
+            if (pos != f) { E.fv[pos] = fv; E.fnx[pos] = nx; E.fny[pos] = ny; E.fnz[pos] = nz; E.fd[pos] = d; }
         }
         base += popc(m);
         __builtin_amdgcn_wave_barrier();
@@ -468,7 +482,8 @@ CTX_T DEV int hull_build(CTX& c, int& nv, int& nf, int m) {
     nf = 4;
     for (int j = 1; j < m; ++j) {
         if (j == i1 || j == i2 || j == i3) continue;
-        int st = hull_add(c, nv, nf, c.vert(j), false, j);
+        bool ch;
+        int st = hull_add(c, nv, nf, c.vert(j), false, j, ch, false);
         if (st) return st;
     }
     return 0;
@@ -521,11 +536,12 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
     auto& E = c.L.u.e;
     const V3<T> O = zero3<T>();
     const int gl = c.g.gl;
-    int nv = 0;
+    int nv = 0, ml_next = 0;
     nf = 0;
     for (int iter = 1;; ++iter) {
         iters = iter;
         if (iter > 99) return GJKEPA_STATUS_EPA_MAXITER;
+        bool unchanged = false;
         int F1;
         T minv;
         V3<T> dir, a1;
@@ -543,16 +559,11 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
             F1 = 4;
         } else {
-            F1 = nf;
-            const int ml = face_argmin(c, nf);
+            F1 = nf;                      // same faces, same order as last iteration's F2: reuse its MINLOC
+            const int ml = ml_next;
             minv = E.fd[ml];
             dir = c.fn(ml);
             a1 = c.vert((int)(E.fv[ml] & 0xffu));
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int f = r * G + gl;
-                if (f < nf) E.dsv[f] = E.fd[f];
-            }
         }
         T dt = dot(vsub(a1, O), dir);
         if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
@@ -597,8 +608,17 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             __builtin_amdgcn_wave_barrier();
             st = hull_build(c, nv, nf, m);
         } else {
-            st = hull_add(c, nv, nf, sp, true, 0);
-            if (!st && two) st = hull_add(c, nv, nf, support(c, vneg(dir)), true, 0);
+            if (two) {                    // net face count of two insertions unknown: save now
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    int f = r * G + gl;
+                    if (f < nf) E.dsv[f] = E.fd[f];
+                }
+            }
+            bool ch1 = false, ch2 = false;
+            st = hull_add(c, nv, nf, sp, true, 0, ch1, !two);
+            if (!st && two) st = hull_add(c, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
+            unchanged = !ch1 && !ch2;
         }
         if (st) return st;
         const int F2 = nf;                                        // :956-969
@@ -606,8 +626,9 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
         const T minv2 = E.fd[ml2];
         V3<T> dir2 = c.fn(ml2);
         if (c.g.unib(dot(vsub(c.vert((int)(E.fv[ml2] & 0xffu)), O), dir2) < T(0))) dir2 = vneg(dir2);
+        ml_next = ml2;
         bool stop;                                                // :972-1015
-        if (F1 == F2) stop = sorted_equal(c, F1);
+        if (F1 == F2) stop = unchanged || sorted_equal(c, F1);   // unchanged hull: identical sorted lists
         else stop = F1 > F2;
         if (stop) { depth = minv2; normal = dir2; return 0; }
     }
@@ -998,10 +1019,16 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
     T depth = 0;
     V3<T> n = O;
     int eit = 0, nf = 0;
+#ifdef GJKEPA_DIAG_GJK_ONLY   // timing ablation only (tools/build_variant.sh); never in the product build
+    return -1;
+#endif
     int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf);
     diag = (uint32_t)(gjk_it & 0xff) | ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
     if (st) return st;
     __builtin_amdgcn_wave_barrier();
+#ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
+    return -1;
+#endif
     int ia, ib;
     support_idx(c, n, ia, ib);                                           // get_nearest_points (:813-855)
     const V3<T> q1 = c.A(ia), q2 = c.B(ib);

@@ -61,7 +61,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("GJKEPA_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise GjkEpaError(f"{p} not built; run `make -C collision-detect-gjk-epa_amd`")
     lib = ctypes.CDLL(p)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build a variant of libgjkepa_hip.so with overridden tier parameters (for A/B timing).
+# usage: tools/build_variant.sh NAME "-DGJKEPA_T0_G=32 -DGJKEPA_T0_K=1 ..."
+set -e
+NAME=$1; shift
+D=collision-detect-gjk-epa_amd
+OUT=$D/build/variants/$NAME
+mkdir -p $OUT
+F="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $*"
+/opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_kernel.hip -o $OUT/k.o
+/opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_capi.cpp -o $OUT/c.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k.o $OUT/c.o $D/build/synth.o -o $OUT/libgjkepa_hip.so
+echo built $OUT/libgjkepa_hip.so
