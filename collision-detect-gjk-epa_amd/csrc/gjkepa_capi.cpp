@@ -3,7 +3,7 @@
 // Host-buffer entries (gjkepa_query, gjkepa_batch) own per-device staging buffers that grow as
 // needed and are reused; they are serialised per device by a mutex, so concurrent callers (the
 // reference's `!$OMP PARALLEL DO ... CALL GJKEPA` pattern) are safe.  gjkepa_batch_device never
-// allocates or synchronises: it enqueues one hipMemsetAsync and three kernels on the stream.
+// allocates or synchronises: it enqueues six kernels (2 GJK + 4 EPA tiers), no atomics.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -79,11 +79,23 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus) {
     if (n_pairs == 0) return 0;
     if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
-    char* ws = (char*)workspace;
-    int32_t* counts = (int32_t*)ws;                      // [t-1]: size of tier t's work list
-    hipError_t e = hipMemsetAsync(counts, 0, kWsHeader, s);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-    gjkepa_tier_args a{};
+    // workspace: one route byte per pair (written by GJK tier 0 for every pair before any read)
+    uint8_t* route = (uint8_t*)workspace + kWsHeader;
+    hipError_t e;
+    gjkepa_gjk_args g{};
+    g.verts = verts;
+    g.hull_off = hull_off;
+    g.hull_cnt = hull_cnt;
+    g.pairs = pairs;
+    g.n_pairs = n_pairs;
+    g.route = route;
+    g.out = out;
+    g.num_cus = num_cus;
+    g.route_code = -1;                                   // GJK tier 0: every pair
+    if ((e = gjkepa_launch_gjk(0, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 0 launch");
+    g.route_code = GJKEPA_ROUTE_GJK1;                    // GJK tier 1: hulls above tier 0's capacity
+    if ((e = gjkepa_launch_gjk(1, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 1 launch");
+    gjkepa_epa_args a{};
     a.version = version;
     a.tol_ff = tol_ff;
     a.verts = verts;
@@ -91,18 +103,13 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.hull_cnt = hull_cnt;
     a.pairs = pairs;
     a.n_pairs = n_pairs;
+    a.route = route;
     a.out = out;
     a.num_cus = num_cus;
-    a.grid = 0;
-    for (int t = 0; t < GJKEPA_NUM_TIERS; ++t) {
-        // tier 0 takes every pair; tier t > 0 the pairs tier t-1 deferred; the last never defers
-        a.in_list = t == 0 ? nullptr : (const int32_t*)(ws + kWsHeader) + (int64_t)(t - 1) * n_pairs;
-        a.in_count = t == 0 ? nullptr : counts + (t - 1);
-        const bool last = t == GJKEPA_NUM_TIERS - 1;
-        a.out_list = last ? nullptr : (int32_t*)(ws + kWsHeader) + (int64_t)t * n_pairs;
-        a.out_count = last ? nullptr : counts + t;
-        e = gjkepa_launch_tier(t, vert_dtype, precision, a, s);
-        if (e != hipSuccess) return hip_fail(e, "tier launch");
+    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {          // EPA tier t; polytope overflow -> t+1
+        a.route_code = GJKEPA_ROUTE_EPA0 + t;
+        a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
+        if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, s)) != hipSuccess) return hip_fail(e, "EPA tier launch");
     }
     return 0;
 }
@@ -124,19 +131,19 @@ int gjkepa_record_bytes(int32_t precision) {
 
 int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
     if (n_pairs < 0) return GJKEPA_E_ARG;
-    return kWsHeader + (GJKEPA_NUM_TIERS - 1) * (int64_t)sizeof(int32_t) * n_pairs;
+    return kWsHeader + n_pairs;
 }
 
 const char* gjkepa_last_error(void) { return g_err.c_str(); }
 
 const char* gjkepa_version_string(void) {
-    static char buf[256];
+    static char buf[512];
     std::snprintf(buf, sizeof(buf),
-                  "gjkepa-mi355x gfx950 wave64; tiers G/K/VCAP/FCAP = %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, "
-                  "%d/%d/%d/%d; -O3 -ffp-contract=off",
-                  GJKEPA_T0_G, GJKEPA_T0_K, GJKEPA_T0_VCAP, GJKEPA_T0_FCAP, GJKEPA_T1_G, GJKEPA_T1_K, GJKEPA_T1_VCAP,
-                  GJKEPA_T1_FCAP, GJKEPA_T2_G, GJKEPA_T2_K, GJKEPA_T2_VCAP, GJKEPA_T2_FCAP, GJKEPA_T3_G, GJKEPA_T3_K,
-                  GJKEPA_T3_VCAP, GJKEPA_T3_FCAP);
+                  "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
+                  "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; -O3 -ffp-contract=off",
+                  GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
+                  GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
+                  GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP);
     return buf;
 }
 

@@ -1,69 +1,114 @@
-// gjkepa_kernel.h — host-side interface of the tiered GJK/EPA kernels (internal, not the C-ABI).
+// gjkepa_kernel.h — host-side interface of the GJK and EPA kernels (internal, not the C-ABI).
 //
-// Tiers: every pair first runs in tier 0 (hulls up to G*K vertices, EPA polytope up to
-// VCAP vertices / FCAP faces).  A pair that does not fit is appended, on the device, to the next
-// tier's work list, and so on; the last tier holds the worst case the reference allows
-// (6 + 2*99 EPA points, 2*V-4 faces), so it never defers.  Deferral recomputes the pair from
-// scratch, so results do not depend on which tier produced them.
+// Two phases, each in tiers.  GJK tier 0 takes every pair (hulls up to G0*K0 vertices; larger
+// hulls go to GJK tier 1).  Misses and errors are final after GJK; each hit is routed to the
+// smallest EPA tier whose hull capacity holds it.  An EPA tier that runs out of polytope capacity
+// (VCAP vertices / FCAP faces) routes the pair to the next EPA tier, which
+// recomputes it from the same GJK simplex; the last EPA tier holds the worst case the reference
+// allows (6 + 2*99 EPA points, 2V-4 faces), so it never defers.  Which tier answered never
+// changes a result.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
 #include <cstdint>
 
-// tier t: G lanes per pair (64/G pairs per wave), K vertices per lane per hull (hull <= G*K),
-// EPA polytope capacity VCAP vertices / FCAP faces
-#ifndef GJKEPA_T0_G
-#define GJKEPA_T0_G 16
+// GJK tiers: G lanes per pair (64/G pairs per wave), K vertices per lane per hull (hull <= G*K)
+#ifndef GJKEPA_G0_G
+#define GJKEPA_G0_G 16
 #endif
-#ifndef GJKEPA_T0_K
-#define GJKEPA_T0_K 2
+#ifndef GJKEPA_G0_K
+#define GJKEPA_G0_K 2
 #endif
-#ifndef GJKEPA_T0_VCAP
-#define GJKEPA_T0_VCAP 40
+#ifndef GJKEPA_G0_MINW
+#define GJKEPA_G0_MINW 3        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
 #endif
-#ifndef GJKEPA_T0_FCAP
-#define GJKEPA_T0_FCAP 64
+#define GJKEPA_G1_G 64
+#define GJKEPA_G1_K 4
+#define GJKEPA_G1_MINW 2
+// EPA tiers: G, K as above, EPA polytope capacity VCAP vertices / FCAP faces
+#ifndef GJKEPA_E0_G
+#define GJKEPA_E0_G 16
 #endif
-#ifndef GJKEPA_T1_G
-#define GJKEPA_T1_G 64
+#ifndef GJKEPA_E0_K
+#define GJKEPA_E0_K 2
 #endif
-#ifndef GJKEPA_T1_K
-#define GJKEPA_T1_K 1
+#ifndef GJKEPA_E0_VCAP
+#define GJKEPA_E0_VCAP 40
 #endif
-#ifndef GJKEPA_T1_VCAP
-#define GJKEPA_T1_VCAP 64
+#ifndef GJKEPA_E0_FCAP
+#define GJKEPA_E0_FCAP 64
 #endif
-#ifndef GJKEPA_T1_FCAP
-#define GJKEPA_T1_FCAP 128
+#ifndef GJKEPA_E0_MINW
+#define GJKEPA_E0_MINW 2
 #endif
-#ifndef GJKEPA_T2_G
-#define GJKEPA_T2_G 64
+#ifndef GJKEPA_E1_G
+#define GJKEPA_E1_G 64
 #endif
-#ifndef GJKEPA_T2_K
-#define GJKEPA_T2_K 4
+#ifndef GJKEPA_E1_K
+#define GJKEPA_E1_K 1
 #endif
-#ifndef GJKEPA_T2_VCAP
-#define GJKEPA_T2_VCAP 104
+#ifndef GJKEPA_E1_VCAP
+#define GJKEPA_E1_VCAP 64
 #endif
-#ifndef GJKEPA_T2_FCAP
-#define GJKEPA_T2_FCAP 208
+#ifndef GJKEPA_E1_FCAP
+#define GJKEPA_E1_FCAP 128
 #endif
-#ifndef GJKEPA_T3_G
-#define GJKEPA_T3_G 64
+#ifndef GJKEPA_E1_MINW
+#define GJKEPA_E1_MINW 2
 #endif
-#ifndef GJKEPA_T3_K
-#define GJKEPA_T3_K 4
+#ifndef GJKEPA_E2_G
+#define GJKEPA_E2_G 64
 #endif
-#ifndef GJKEPA_T3_VCAP
-#define GJKEPA_T3_VCAP 208
+#ifndef GJKEPA_E2_K
+#define GJKEPA_E2_K 4
 #endif
-#ifndef GJKEPA_T3_FCAP
-#define GJKEPA_T3_FCAP 416
+#ifndef GJKEPA_E2_VCAP
+#define GJKEPA_E2_VCAP 104
 #endif
-#define GJKEPA_NUM_TIERS 4
+#ifndef GJKEPA_E2_FCAP
+#define GJKEPA_E2_FCAP 208
+#endif
+#ifndef GJKEPA_E2_MINW
+#define GJKEPA_E2_MINW 1
+#endif
+#ifndef GJKEPA_E3_G
+#define GJKEPA_E3_G 64
+#endif
+#ifndef GJKEPA_E3_K
+#define GJKEPA_E3_K 4
+#endif
+#ifndef GJKEPA_E3_VCAP
+#define GJKEPA_E3_VCAP 208
+#endif
+#ifndef GJKEPA_E3_FCAP
+#define GJKEPA_E3_FCAP 416
+#endif
+#ifndef GJKEPA_E3_MINW
+#define GJKEPA_E3_MINW 1
+#endif
+#define GJKEPA_GJK_TIERS 2
+#define GJKEPA_EPA_TIERS 4
 
-struct gjkepa_tier_args {
+// route byte per pair (workspace): which kernel owns the pair next
+#define GJKEPA_ROUTE_DONE 0
+#define GJKEPA_ROUTE_GJK1 1
+#define GJKEPA_ROUTE_EPA0 0x10      // + EPA tier
+
+struct gjkepa_gjk_args {
+    const void* verts;
+    const int64_t* hull_off;
+    const int32_t* hull_cnt;
+    const int32_t* pairs;
+    int64_t n_pairs;
+    uint8_t* route;             // [n_pairs]
+    int route_code;             // pairs this launch serves: -1 = all (tier 0), else route code
+    void* out;                  // contact records (hits: simplex codes parked in their slot)
+    int grid;                   // <= 0: occupancy x CUs
+    int num_cus;
+};
+
+struct gjkepa_epa_args {
     int version;
     double tol_ff;
     const void* verts;
@@ -71,13 +116,13 @@ struct gjkepa_tier_args {
     const int32_t* hull_cnt;
     const int32_t* pairs;
     int64_t n_pairs;
-    const int32_t* in_list;    // null: process pairs [0, n_pairs)
-    const int32_t* in_count;   // device count of in_list
-    int32_t* out_list;         // null on the last tier
-    int32_t* out_count;
-    void* out;                 // contact records
-    int grid;                  // <= 0: occupancy x CUs
+    uint8_t* route;
+    int route_code;             // GJKEPA_ROUTE_EPA0 + tier
+    int next_code;              // route code for polytope overflow; -1 on the last tier
+    void* out;
+    int grid;
     int num_cus;
 };
 
-hipError_t gjkepa_launch_tier(int tier, int vert_dtype, int precision, const gjkepa_tier_args& a, hipStream_t s);
+hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s);
+hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);

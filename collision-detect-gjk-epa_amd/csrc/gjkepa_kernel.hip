@@ -284,32 +284,6 @@ template <typename T> DEV bool origin_in_simplex(V3<T> s0, V3<T> s1, V3<T> s2, V
     if (fabs(d3) < Tol<T>::PT && inside_tri(s1, s2, s3, O)) return true;
     return d0 > T(0) && d1 > T(0) && d2 > T(0) && d3 > T(0);
 }
-// update_simplex_GJK (:1070-1157): MAXLOC of the signed outside distances (first max), support
-// along that face's normal, keep the face's vertices.
-CTX_T DEV void update_simplex(const CTX& c, V3<T>& s0, V3<T>& s1, V3<T>& s2, V3<T>& s3) {
-    const V3<T> M = centroid4(s0, s1, s2, s3), O = zero3<T>();
-    V3<T> n0 = face_nml(s0, s2, s3), n1 = face_nml(s0, s1, s3), n2 = face_nml(s0, s1, s2), n3 = face_nml(s1, s2, s3);
-    if (dot(n0, vsub(s0, M)) < T(0)) n0 = vneg(n0);
-    if (dot(n1, vsub(s0, M)) < T(0)) n1 = vneg(n1);
-    if (dot(n2, vsub(s0, M)) < T(0)) n2 = vneg(n2);
-    if (dot(n3, vsub(s1, M)) < T(0)) n3 = vneg(n3);
-    const T d0 = dot(vneg(n0), vsub(s0, O)), d1 = dot(vneg(n1), vsub(s0, O));
-    const T d2 = dot(vneg(n2), vsub(s0, O)), d3 = dot(vneg(n3), vsub(s1, O));
-    int k = 0;
-    T best = d0;
-    V3<T> dir = n0;
-    if (d1 > best) { best = d1; k = 1; dir = n1; }
-    if (d2 > best) { best = d2; k = 2; dir = n2; }
-    if (d3 > best) { best = d3; k = 3; dir = n3; }
-    k = c.g.uni(k);
-    const V3<T> SM = support(c, dir);
-    const V3<T> o0 = s0, o1 = s1, o2 = s2, o3 = s3;
-    s0 = vsel(k == 3, o1, o0);
-    s1 = vsel(k == 0 || k == 3, o2, o1);
-    s2 = vsel(k == 2, o2, o3);
-    s3 = SM;
-}
-
 // ---------------------------------------------------------------- EPA polytope (re-supplied hull)
 CTX_T DEV void write_face(CTX& c, int f, int a, int b, int d, V3<T> n, T dist) {
     auto& E = c.L.u.e;
@@ -929,14 +903,61 @@ CTX_T DEV int contact_v3(CTX& c, V3<T> n, V3<T>& res, V3<T>& nnew) {
     return 0;
 }
 
-// ---------------------------------------------------------------- one pair (GJKEPA :39-239)
-// returns: 0 no hit, -type for an OK hit (o13 filled), > 0 error status, ST_DEFER
-CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint32_t& diag) {
+// ---------------------------------------------------------------- GJK phase (GJKEPA :39-239)
+// A simplex vertex is a Minkowski point A[ia] - B[ib]; it is carried as the code ia | ib << 16 so
+// the EPA kernel can rebuild it bit for bit.  kStale encodes the never-assigned row 4 (= 0).
+constexpr uint32_t kStale = 0xFFFFFFFFu;
+constexpr int PH_MISS = 0, PH_HIT = -1;
+
+CTX_T DEV V3<T> support_pt(const CTX& c, V3<T> d, uint32_t& code) {
+    int ia, ib;
+    support_idx(c, d, ia, ib);
+    code = (uint32_t)ia | ((uint32_t)ib << 16);
+    return vsub(c.A(ia), c.B(ib));
+}
+CTX_T DEV V3<T> decode_pt(const CTX& c, uint32_t code) {
+    if (code == kStale) return zero3<T>();
+    return vsub(c.A((int)(code & 0xffffu)), c.B((int)(code >> 16)));
+}
+
+// update_simplex_GJK (:1070-1157) with vertex codes carried along
+CTX_T DEV void update_simplex_c(const CTX& c, V3<T>& s0, V3<T>& s1, V3<T>& s2, V3<T>& s3,
+                                uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+    const V3<T> M = centroid4(s0, s1, s2, s3), O = zero3<T>();
+    V3<T> n0 = face_nml(s0, s2, s3), n1 = face_nml(s0, s1, s3), n2 = face_nml(s0, s1, s2), n3 = face_nml(s1, s2, s3);
+    if (dot(n0, vsub(s0, M)) < T(0)) n0 = vneg(n0);
+    if (dot(n1, vsub(s0, M)) < T(0)) n1 = vneg(n1);
+    if (dot(n2, vsub(s0, M)) < T(0)) n2 = vneg(n2);
+    if (dot(n3, vsub(s1, M)) < T(0)) n3 = vneg(n3);
+    const T d0 = dot(vneg(n0), vsub(s0, O)), d1 = dot(vneg(n1), vsub(s0, O));
+    const T d2 = dot(vneg(n2), vsub(s0, O)), d3 = dot(vneg(n3), vsub(s1, O));
+    int k = 0;
+    T best = d0;
+    V3<T> dir = n0;
+    if (d1 > best) { best = d1; k = 1; dir = n1; }
+    if (d2 > best) { best = d2; k = 2; dir = n2; }
+    if (d3 > best) { best = d3; k = 3; dir = n3; }
+    k = c.g.uni(k);
+    uint32_t km;
+    const V3<T> SM = support_pt(c, dir, km);
+    const V3<T> o0 = s0, o1 = s1, o2 = s2;
+    const uint32_t c0 = k0, c1 = k1, c2 = k2, c3 = k3;
+    s0 = vsel(k == 3, o1, o0);
+    s1 = vsel(k == 0 || k == 3, o2, o1);
+    s2 = vsel(k == 2, o2, s3);
+    s3 = SM;
+    k0 = k == 3 ? c1 : c0;
+    k1 = (k == 0 || k == 3) ? c2 : c1;
+    k2 = k == 2 ? c2 : c3;
+    k3 = km;
+}
+
+// Sphere pre-test + GJK.  Returns PH_MISS, PH_HIT (codes k0..k3 filled) or an error status.
+CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     const V3<T> O = zero3<T>();
-    hit = 0;
-    diag = 0;
     auto& L = c.L;
     const int gl = c.g.gl;
+    gjk_it = 0;
     {   // RoughCollisionDetection_SphericalEnvelope (:1165-1188)
         T s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0, t2 = 0;
         for (int i = 0; i < c.na; ++i) { s0 += (T)L.hx[0][i]; s1 += (T)L.hy[0][i]; s2 += (T)L.hz[0][i]; }
@@ -954,33 +975,33 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
         }
         r1 = gmax<G>(r1);
         r2 = gmax<G>(r2);
-        if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return 0;
+        if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
     }
     // --- initial simplex (:82-170)
     V3<T> s0 = O, s1 = O, s2 = O, s3 = O;   // fresh SAVE state: stale row 4 = 0
+    uint32_t k0 = kStale, k1 = kStale, k2 = kStale, k3 = kStale;
     V3<T> dir;
     for (int iter = 1;; ++iter) {
-        if (iter > 99) return 0;
+        if (iter > 99) return PH_MISS;
         dir = vmk<T>((T)kDirTab[iter - 1][0], (T)kDirTab[iter - 1][1], (T)kDirTab[iter - 1][2]);
-        s0 = support(c, dir);
+        s0 = support_pt(c, dir, k0);
         dir = vneg(dir);
-        s1 = support(c, dir);
+        s1 = support_pt(c, dir, k1);
         if (!c.g.unib(allclose8(s0, s1))) break;
     }
     dir = vec_pl(O, s0, s1);
-    s2 = support(c, dir);
-    if (c.g.unib(allclose8(s2, s0) || allclose8(s2, s1))) return 0;
+    s2 = support_pt(c, dir, k2);
+    if (c.g.unib(allclose8(s2, s0) || allclose8(s2, s1))) return PH_MISS;
     dir = utzvec(cross(vsub(s1, s0), vsub(s2, s1)));
     const T vd = dot(vsub(O, s2), dir);
-    int gjk_it = 0;
     bool enter = false;
     if (c.g.unib(fabs(vd) < Tol<T>::PT) && c.g.unib(inside_tri(s0, s1, s2, O))) enter = true;
     if (!enter) {
         if (c.g.unib(vd < T(0))) dir = vneg(dir);
-        s3 = support(c, dir);
+        s3 = support_pt(c, dir, k3);
         const V3<T> n = uninml(s0, s1, s2);                         // DIST_PF_SIGN (:157)
-        if (c.g.unib(is_zero_nml(n))) { hit = 1; return GJKEPA_STATUS_DEGENERATE; }
-        if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return 0;
+        if (c.g.unib(is_zero_nml(n))) return GJKEPA_STATUS_DEGENERATE;
+        if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return PH_MISS;
         if (c.g.unib(origin_in_simplex(s0, s1, s2, s3))) enter = true;
     }
     if (!enter) {
@@ -988,7 +1009,7 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
         if (gl < 12) { H.l1[gl] = T(0); H.l2[gl] = T(0); }
         for (int it = 1;; ++it) {                                        // :182-236
             gjk_it = it;
-            if (it > 50) return 0;
+            if (it > 50) return PH_MISS;
             // history: last2 = last1, last1 = simplex (:193-194); group lane j owns coordinate j
             __builtin_amdgcn_wave_barrier();
             if (gl < 12) {
@@ -998,11 +1019,11 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
                 H.l1[gl] = cc == 0 ? q.x : cc == 1 ? q.y : q.z;
             }
             __builtin_amdgcn_wave_barrier();
-            update_simplex(c, s0, s1, s2, s3);
-            if (c.g.unib(norm2(cross(vsub(s1, s0), vsub(s2, s1))) < Tol<T>::PT)) return 0;   // :199-201
+            update_simplex_c(c, s0, s1, s2, s3, k0, k1, k2, k3);
+            if (c.g.unib(norm2(cross(vsub(s1, s0), vsub(s2, s1))) < Tol<T>::PT)) return PH_MISS;   // :199-201
             const V3<T> n = uninml(s0, s1, s2);
-            if (c.g.unib(is_zero_nml(n))) { hit = 1; diag = (uint32_t)gjk_it; return GJKEPA_STATUS_DEGENERATE; }
-            if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return 0;             // :203-206
+            if (c.g.unib(is_zero_nml(n))) return GJKEPA_STATUS_DEGENERATE;
+            if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return PH_MISS;         // :203-206
             if (c.g.unib(origin_in_simplex(s0, s1, s2, s3))) break;                       // :210-216
             const V3<T> l10 = vmk<T>(H.l1[0], H.l1[1], H.l1[2]), l11 = vmk<T>(H.l1[3], H.l1[4], H.l1[5]);
             const V3<T> l12 = vmk<T>(H.l1[6], H.l1[7], H.l1[8]), l13 = vmk<T>(H.l1[9], H.l1[10], H.l1[11]);
@@ -1010,35 +1031,41 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
             const V3<T> l22 = vmk<T>(H.l2[6], H.l2[7], H.l2[8]), l23 = vmk<T>(H.l2[9], H.l2[10], H.l2[11]);
             const bool over = (allclose8(s0, l10) || allclose8(s0, l20)) && (allclose8(s1, l11) || allclose8(s1, l21)) &&
                               (allclose8(s2, l12) || allclose8(s2, l22)) && (allclose8(s3, l13) || allclose8(s3, l23));
-            if (c.g.unib(over)) return 0;                                                 // :219-234
+            if (c.g.unib(over)) return PH_MISS;                                           // :219-234
         }
         __builtin_amdgcn_wave_barrier();
     }
-    // --- EPA_solu (:242-346)
-    hit = 1;
+    kc[0] = k0; kc[1] = k1; kc[2] = k2; kc[3] = k3;
+    return PH_HIT;
+}
+
+// EPA_solu (:242-346) from the GJK simplex.  Returns -type (OK, o13 filled), an error status or
+// ST_DEFER; `diag_epa` gets (epa_iters << 8) | (faces << 16).
+CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, int version, T tol_ff, T* o13, uint32_t& diag_epa) {
+    const V3<T> s0 = decode_pt(c, kc[0]), s1 = decode_pt(c, kc[1]), s2 = decode_pt(c, kc[2]), s3 = decode_pt(c, kc[3]);
     T depth = 0;
-    V3<T> n = O;
+    V3<T> n = zero3<T>();
     int eit = 0, nf = 0;
 #ifdef GJKEPA_DIAG_GJK_ONLY   // timing ablation only (tools/build_variant.sh); never in the product build
     return -1;
 #endif
     int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf);
-    diag = (uint32_t)(gjk_it & 0xff) | ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
+    diag_epa = ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
     if (st) return st;
     __builtin_amdgcn_wave_barrier();
 #ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
     return -1;
 #endif
     int ia, ib;
-    support_idx(c, n, ia, ib);                                           // get_nearest_points (:813-855)
-    const V3<T> q1 = c.A(ia), q2 = c.B(ib);
-    V3<T> pt = O;
-    if (version == 1) st = contact_v1(c, n, pt);
+    support_idx(c, n, ia, ib);                                           // get_nearest_points (:326, :813-855)
+    V3<T> pt = zero3<T>();
+    if (version == 1) st = contact_v1(c, n, pt);                          // :329-340
     else if (version == 2) st = contact_v2(c, n, pt);
     else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; }
     else st = GJKEPA_STATUS_BAD_VERSION;
     if (st) return st;
     const int type = collision_type(c, n, tol_ff);                        // :343
+    const V3<T> q1 = c.A(ia), q2 = c.B(ib);
     o13[0] = depth;
     o13[1] = n.x; o13[2] = n.y; o13[3] = n.z;
     o13[4] = pt.x; o13[5] = pt.y; o13[6] = pt.z;
@@ -1047,109 +1074,178 @@ CTX_T DEV int gjkepa_pair(CTX& c, int version, T tol_ff, T* o13, int& hit, uint3
     return -type;
 }
 
-// ---------------------------------------------------------------- kernel
-template <typename TIn, typename T, int G, int K, int VC, int FC>
-__global__ __launch_bounds__(64, 2) void gjkepa_tier_kernel(
-    int version, double tol_ff, const TIn* __restrict__ verts, const int64_t* __restrict__ hull_off,
-    const int32_t* __restrict__ hull_cnt, const int32_t* __restrict__ pairs, int64_t n_pairs,
-    const int32_t* __restrict__ in_list, const int32_t* __restrict__ in_count,
-    int32_t* __restrict__ out_list, int32_t* __restrict__ out_count, void* __restrict__ out) {
-    using L_t = Lds<T, TIn, G, K, VC, FC>;
-    constexpr int GPW = 64 / G;   // groups (pairs) per wave
+// ---------------------------------------------------------------- kernels
+// Hull load: coalesced SoA loads into registers (compute precision) and the LDS copy.
+CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restrict__ pb) {
+    const int gl = c.g.gl;
+    bool nonfinite = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + gl;
+        TH ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
+        if (i < c.na) { ax = pa[i]; ay = pa[c.na + i]; az = pa[2 * c.na + i]; }
+        if (i < c.nb) { bx = pb[i]; by = pb[c.nb + i]; bz = pb[2 * c.nb + i]; }
+        nonfinite = nonfinite || !isfinite(ax) || !isfinite(ay) || !isfinite(az) || !isfinite(bx) ||
+                    !isfinite(by) || !isfinite(bz);
+        c.ax[k] = (T)ax; c.ay[k] = (T)ay; c.az[k] = (T)az;
+        c.bx[k] = (T)bx; c.by[k] = (T)by; c.bz[k] = (T)bz;
+        c.L.hx[0][i] = ax; c.L.hy[0][i] = ay; c.L.hz[0][i] = az;
+        c.L.hx[1][i] = bx; c.L.hy[1][i] = by; c.L.hz[1][i] = bz;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return c.g.any(nonfinite);
+}
+
+// record: 13 T fields, then int8 collision, type, status, reserved, uint32 diag, zero pad.
+// Group lane j < 16 stores one 8-byte (f64) / 4-byte (f32) word straight from registers.
+template <typename T> DEV void store_record(void* out, int64_t pair, int gl, const T* o13, int hit, int type,
+                                            int status, uint32_t diag) {
+    if (gl >= 16) return;
+    T v = T(0);
+#pragma unroll
+    for (int j = 0; j < 13; ++j) v = (gl == j) ? o13[j] : v;
+    const uint32_t flags = (uint32_t)(hit & 0xff) | ((uint32_t)(type & 0xff) << 8) | ((uint32_t)(status & 0xff) << 16);
+    if constexpr (sizeof(T) == 8) {
+        uint64_t word = __builtin_bit_cast(uint64_t, v);
+        if (gl == 13) word = (uint64_t)flags | ((uint64_t)diag << 32);
+        if (gl > 13) word = 0;
+        reinterpret_cast<uint64_t*>(out)[pair * 16 + gl] = word;
+    } else {
+        uint32_t word = __builtin_bit_cast(uint32_t, v);
+        if (gl == 13) word = flags;
+        if (gl == 14) word = diag;
+        if (gl == 15) word = 0;
+        reinterpret_cast<uint32_t*>(out)[pair * 16 + gl] = word;
+    }
+}
+
+DEV int epa_tier_for(int nmax) { return nmax <= GJKEPA_E0_G * GJKEPA_E0_K ? 0 : nmax <= GJKEPA_E1_G * GJKEPA_E1_K ? 1 : 2; }
+
+// Work distribution without atomics: every pair has a route byte (which kernel owns it next).  A
+// wave scans 64 consecutive route bytes with one coalesced load, ballots the matches and hands
+// them to its 64/G groups in pair order, one per group per round.  `route_code` < 0: every pair.
+// F(pair) runs for each pair the calling group receives.
+template <int G, typename F>
+DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code, F&& f) {
+    constexpr int GPW = 64 / G;
+    const int gid = grp.lane / G;
+    const int64_t nchunks = (n_pairs + 63) / 64;
+    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const int64_t p0 = ch * 64;
+        uint64_t m;
+        if (route_code < 0) {
+            const int64_t left = n_pairs - p0;
+            m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+        } else {
+            const int64_t p = p0 + grp.lane;
+            m = __ballot(p < n_pairs && (int)route[p] == route_code);
+        }
+        while (m) {
+            // group g takes the g-th lowest set bit of m
+            uint64_t mm = m;
+            for (int j = 0; j < gid && mm; ++j) mm &= mm - 1;
+            const bool active = mm != 0;
+            const int bit = active ? (int)__builtin_ctzll(mm) : 0;
+            for (int j = 0; j < GPW && m; ++j) m &= m - 1;   // consume this round's GPW matches
+            if (active) f(p0 + bit);
+        }
+    }
+}
+
+// GJK kernel: sphere pre-test + GJK.  Misses and errors get their final record here; hits park the
+// simplex codes (5 words) in their own record slot and are routed to the smallest EPA tier that
+// holds their hulls.  Tier 0 takes every pair; hulls above its capacity are routed to tier 1.
+template <typename TIn, typename T, int G, int K, int MINW>
+__global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) {
+    using L_t = Lds<T, TIn, G, K, 4, 4>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
-    const int gid = grp.lane / G;
-    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * gid);
+    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
     const int gl = grp.gl;
-    const int64_t total = in_list ? (int64_t)(*in_count) : n_pairs;
-    for (int64_t w = (int64_t)blockIdx.x * GPW + gid; w < total; w += (int64_t)gridDim.x * GPW) {
-        const int64_t pair = in_list ? (int64_t)in_list[w] : w;
-        Ctx<T, TIn, G, K, VC, FC> c{L, grp};
-        const int32_t ha = pairs[2 * pair], hb = pairs[2 * pair + 1];
-        const int na = grp.uni(hull_cnt[ha]), nb = grp.uni(hull_cnt[hb]);
-        int status = 0, hit = 0, type = 0;
-        uint32_t diag = 0;
+    const TIn* verts = (const TIn*)a.verts;
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+        Ctx<T, TIn, G, K, 4, 4> c{L, grp};
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
         T o13[13];
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
-        bool defer = false;
+        uint8_t next = 0;
         if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
-            status = GJKEPA_STATUS_BAD_INPUT;
+            store_record<T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
         } else if (na > K * G || nb > K * G) {
-            defer = true;
+            next = GJKEPA_ROUTE_GJK1;                        // larger GJK tier
         } else {
-            const TIn* pa = verts + hull_off[ha];
-            const TIn* pb = verts + hull_off[hb];
             c.na = na;
             c.nb = nb;
-            bool nonfinite = false;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int i = k * G + gl;
-                TIn ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
-                if (i < na) { ax = pa[i]; ay = pa[na + i]; az = pa[2 * na + i]; }
-                if (i < nb) { bx = pb[i]; by = pb[nb + i]; bz = pb[2 * nb + i]; }
-                nonfinite = nonfinite || !isfinite(ax) || !isfinite(ay) || !isfinite(az) || !isfinite(bx) ||
-                            !isfinite(by) || !isfinite(bz);
-                c.ax[k] = (T)ax; c.ay[k] = (T)ay; c.az[k] = (T)az;
-                c.bx[k] = (T)bx; c.by[k] = (T)by; c.bz[k] = (T)bz;
-                L.hx[0][i] = ax; L.hy[0][i] = ay; L.hz[0][i] = az;
-                L.hx[1][i] = bx; L.hy[1][i] = by; L.hz[1][i] = bz;
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (grp.any(nonfinite)) {
-                status = GJKEPA_STATUS_BAD_INPUT;
+            if (load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb])) {
+                store_record<T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
             } else {
-                const int r = gjkepa_pair(c, version, (T)tol_ff, o13, hit, diag);
-                if (r == ST_DEFER) {
-                    defer = true;
-                } else if (r < 0) {
-                    type = -r;
-                } else if (r > 0) {                 // error status: outputs zero, collision = 1
-                    status = r;
-                    hit = 1;
-#pragma unroll
-                    for (int i = 0; i < 13; ++i) o13[i] = T(0);
+                uint32_t kc[4];
+                int gjk_it = 0;
+                const int r = gjk_phase(c, kc, gjk_it);
+                __builtin_amdgcn_wave_barrier();
+                if (r == PH_HIT) {
+                    if (gl < 5) {
+                        const uint32_t word = gl == 0 ? kc[0] : gl == 1 ? kc[1] : gl == 2 ? kc[2] : gl == 3 ? kc[3] : (uint32_t)gjk_it;
+                        reinterpret_cast<uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + gl] = word;
+                    }
+                    next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(na > nb ? na : nb));
+                } else if (r == PH_MISS) {
+                    store_record<T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
+                } else {                                  // GJK-phase error (reference would STOP)
+                    store_record<T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
                 }
             }
         }
+        if (gl == 0) a.route[pair] = next;
         __builtin_amdgcn_wave_barrier();
-        if (defer && !out_list) {                   // last tier: capacity exhausted
-            defer = false;
-            status = GJKEPA_STATUS_DEGENERATE;
-            hit = 1;
+    });
+}
+
+// EPA kernel: EPA + contact features for the pairs routed to this tier.  A polytope that outgrows
+// the tier is routed to the next one (recomputed from the same simplex codes).
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW>
+__global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) {
+    using L_t = Lds<T, TIn, G, K, VC, FC>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<G> grp;
+    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    const int gl = grp.gl;
+    const TIn* verts = (const TIn*)a.verts;
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+        Ctx<T, TIn, G, K, VC, FC> c{L, grp};
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        c.na = grp.uni(a.hull_cnt[ha]);
+        c.nb = grp.uni(a.hull_cnt[hb]);
+        const uint32_t* slot = reinterpret_cast<const uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
+        uint32_t kc[4];
+        kc[0] = slot[0]; kc[1] = slot[1]; kc[2] = slot[2]; kc[3] = slot[3];
+        const uint32_t gjk_it = slot[4];
+        load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+        T o13[13];
+#pragma unroll
+        for (int i = 0; i < 13; ++i) o13[i] = T(0);
+        uint32_t de = 0;
+        const int r = epa_phase(c, kc, a.version, (T)a.tol_ff, o13, de);
+        __builtin_amdgcn_wave_barrier();
+        uint8_t next = 0;
+        if (r == ST_DEFER && a.next_code >= 0) {
+            next = (uint8_t)a.next_code;
+        } else if (r == ST_DEFER) {                       // last tier: capacity exhausted
 #pragma unroll
             for (int i = 0; i < 13; ++i) o13[i] = T(0);
-        }
-        if (defer) {
-            if (gl == 0) {
-                const int pos = atomicAdd(out_count, 1);
-                out_list[pos] = (int32_t)pair;
-            }
-            continue;
-        }
-        // record: 13 T fields, then int8 collision, type, status, reserved, uint32 diag, zero pad.
-        // Group lane j < 16 stores one 8-byte (f64) / 4-byte (f32) word straight from registers.
-        if (gl < 16) {
-            T v = T(0);
+            store_record<T>(a.out, pair, gl, o13, 1, 0, GJKEPA_STATUS_DEGENERATE, (gjk_it & 0xffu) | de);
+        } else if (r < 0) {
+            store_record<T>(a.out, pair, gl, o13, 1, -r, 0, (gjk_it & 0xffu) | de);
+        } else {                                          // error status: outputs zero, collision = 1
 #pragma unroll
-            for (int j = 0; j < 13; ++j) v = (gl == j) ? o13[j] : v;
-            const uint32_t flags = (uint32_t)(hit & 0xff) | ((uint32_t)(type & 0xff) << 8) | ((uint32_t)(status & 0xff) << 16);
-            if constexpr (sizeof(T) == 8) {
-                uint64_t word = __builtin_bit_cast(uint64_t, v);
-                if (gl == 13) word = (uint64_t)flags | ((uint64_t)diag << 32);
-                if (gl > 13) word = 0;
-                reinterpret_cast<uint64_t*>(out)[pair * 16 + gl] = word;
-            } else {
-                uint32_t word = __builtin_bit_cast(uint32_t, v);
-                if (gl == 13) word = flags;
-                if (gl == 14) word = diag;
-                if (gl == 15) word = 0;
-                reinterpret_cast<uint32_t*>(out)[pair * 16 + gl] = word;
-            }
+            for (int i = 0; i < 13; ++i) o13[i] = T(0);
+            store_record<T>(a.out, pair, gl, o13, 1, 0, r, (gjk_it & 0xffu) | de);
         }
+        if (gl == 0) a.route[pair] = next;
         __builtin_amdgcn_wave_barrier();
-    }
+    });
 }
 
 }  // namespace gk
@@ -1157,47 +1253,64 @@ __global__ __launch_bounds__(64, 2) void gjkepa_tier_kernel(
 // ---------------------------------------------------------------- host-side launch table
 namespace {
 
-template <typename TIn, typename T, int G, int K, int VC, int FC>
-hipError_t launch_tier(const gjkepa_tier_args& a, hipStream_t s) {
-    using Img = gk::Lds<T, TIn, G, K, VC, FC>;
-    auto kfn = gk::gjkepa_tier_kernel<TIn, T, G, K, VC, FC>;
+template <typename K_t> int grid_for(K_t kfn, size_t lds, int num_cus, int grid) {
+    if (grid > 0) return grid;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    return per_cu * num_cus;
+}
+
+template <typename TIn, typename T, int G, int K, int MINW>
+hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
+    auto kfn = gk::gjk_kernel<TIn, T, G, K, MINW>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(Img) * GPW;
-    int grid = a.grid;
-    if (grid <= 0) {
-        int per_cu = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds);
-        if (e != hipSuccess) return e;
-        if (per_cu < 1) per_cu = 1;
-        grid = per_cu * a.num_cus;
-    }
-    if (!a.in_list) {
-        const int64_t need = (a.n_pairs + GPW - 1) / GPW;
-        if (need < grid) grid = (int)(need > 0 ? need : 1);
-    }
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a.version, a.tol_ff, (const TIn*)a.verts,
-                       a.hull_off, a.hull_cnt, a.pairs, a.n_pairs, a.in_list, a.in_count, a.out_list,
-                       a.out_count, a.out);
+    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 4, 4>) * GPW;
+    int grid = grid_for(kfn, lds, a.num_cus, a.grid);
+    const int64_t chunks = (a.n_pairs + 63) / 64;
+    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
 
-#define TIER_ARGS(t) GJKEPA_T##t##_G, GJKEPA_T##t##_K, GJKEPA_T##t##_VCAP, GJKEPA_T##t##_FCAP
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW>
+hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
+    auto kfn = gk::epa_kernel<TIn, T, G, K, VC, FC, MINW>;
+    constexpr int GPW = 64 / G;
+    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, VC, FC>) * GPW;
+    int grid = grid_for(kfn, lds, a.num_cus, a.grid);
+    const int64_t chunks = (a.n_pairs + 63) / 64;
+    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
+    return hipGetLastError();
+}
+
+#define EPA_ARGS(t) GJKEPA_E##t##_G, GJKEPA_E##t##_K, GJKEPA_E##t##_VCAP, GJKEPA_E##t##_FCAP, GJKEPA_E##t##_MINW
 
 template <typename TIn, typename T>
-hipError_t launch_any(int tier, const gjkepa_tier_args& a, hipStream_t s) {
+hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
+    return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW>(a, s)
+                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW>(a, s);
+}
+template <typename TIn, typename T>
+hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
-        case 0: return launch_tier<TIn, T, TIER_ARGS(0)>(a, s);
-        case 1: return launch_tier<TIn, T, TIER_ARGS(1)>(a, s);
-        case 2: return launch_tier<TIn, T, TIER_ARGS(2)>(a, s);
-        default: return launch_tier<TIn, T, TIER_ARGS(3)>(a, s);
+        case 0: return launch_epa<TIn, T, EPA_ARGS(0)>(a, s);
+        case 1: return launch_epa<TIn, T, EPA_ARGS(1)>(a, s);
+        case 2: return launch_epa<TIn, T, EPA_ARGS(2)>(a, s);
+        default: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
     }
 }
 
 }  // namespace
 
-hipError_t gjkepa_launch_tier(int tier, int vert_dtype, int precision, const gjkepa_tier_args& a, hipStream_t s) {
-    if (vert_dtype == GJKEPA_DTYPE_F32) {
-        return precision == GJKEPA_PREC_F64 ? launch_any<float, double>(tier, a, s) : launch_any<float, float>(tier, a, s);
-    }
-    return precision == GJKEPA_PREC_F64 ? launch_any<double, double>(tier, a, s) : launch_any<double, float>(tier, a, s);
+hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s) {
+    if (vert_dtype == GJKEPA_DTYPE_F32)
+        return precision == GJKEPA_PREC_F64 ? gjk_any<float, double>(tier, a, s) : gjk_any<float, float>(tier, a, s);
+    return precision == GJKEPA_PREC_F64 ? gjk_any<double, double>(tier, a, s) : gjk_any<double, float>(tier, a, s);
+}
+
+hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
+    if (vert_dtype == GJKEPA_DTYPE_F32)
+        return precision == GJKEPA_PREC_F64 ? epa_any<float, double>(tier, a, s) : epa_any<float, float>(tier, a, s);
+    return precision == GJKEPA_PREC_F64 ? epa_any<double, double>(tier, a, s) : epa_any<double, float>(tier, a, s);
 }
