@@ -26,16 +26,25 @@ sys.path.insert(0, os.path.join(ROOT, "collision-detect-gjk-epa_amd"))
 import numpy as np  # noqa: E402
 
 import gjkepa  # noqa: E402
+import shard  # noqa: E402
 
 SEED = 0x6A4B5C1D
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "M convex-pair GJK+EPA queries/sec at 1/2/4/8 MI355X; % HBM roofline"
 
 
-def algorithmic_bytes_per_query(n1: int, n2: int, vert_bytes: int, rec_bytes: int) -> int:
+# BASELINE.json configs: (hull n_min, n_max, centre offset r_max, default pairs per GPU)
+CONFIGS = {
+    "C2": (32, 32, 2.5, 1 << 20, "1M random 32-vertex convex-hull pairs"),
+    "C4": (8, 256, 2.5, 4 << 20, "4M pairs, mixed hull sizes 8-256 vertices"),
+    "C5": (32, 128, 0.3, 1 << 20, "deep-overlap pairs (r~U[0,0.3]), 32-128-vertex hulls, EPA-heavy"),
+}
+
+
+def algorithmic_bytes_per_query(mean_verts_per_pair: float, vert_bytes: int, rec_bytes: int) -> float:
     """Bytes one query must move through HBM: both hulls' vertices (SoA), the pair's two hull
-    indices, the two hulls' (offset, count) and the contact record it writes (DESIGN.md §Roofline)."""
-    return vert_bytes * 3 * (n1 + n2) + 2 * 4 + 2 * (8 + 4) + rec_bytes
+    indices, the two hulls' (offset, count) and the contact record it writes (DESIGN.md §5)."""
+    return vert_bytes * 3 * mean_verts_per_pair + 2 * 4 + 2 * (8 + 4) + rec_bytes
 
 
 def parse():
@@ -43,15 +52,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs-per-gpu", type=int, default=1 << 20)
-    ap.add_argument("--nverts", type=int, default=32)
-    ap.add_argument("--rmax", type=float, default=2.5)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
+    ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: the config's size")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--version", type=int, default=2)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather for N>1")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 18)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="pairs for the CPU baseline (0: the whole batch)")
     return ap.parse_args()
 
 
@@ -68,17 +77,23 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))   # gloo rehearsal: ranks may share a GPU
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    host_coll = dist is not None and args.backend != "nccl"     # gloo: collectives staged through host memory
     lib = gjkepa.load()
 
-    n = args.pairs_per_gpu
+    nmin, nmax, rmax, n_default, desc = CONFIGS[args.config]
+    n = args.pairs_per_gpu or n_default
     prec = gjkepa.PREC_F64 if args.precision == "f64" else gjkepa.PREC_F32
     rec_bytes = lib.gjkepa_record_bytes(prec)
-    pool = gjkepa.synth_pairs(SEED, n, args.nverts, args.nverts, args.rmax, first_pair=rank * n, dtype=np.float32)
+    first, _ = shard.shard_range(n * world, world, rank)
+    pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax, first_pair=first, dtype=np.float32)
     verts = torch.from_numpy(pool.verts).to(dev)
     off = torch.from_numpy(pool.hull_off).to(dev)
     cnt = torch.from_numpy(pool.hull_cnt).to(dev)
@@ -105,7 +120,12 @@ def main():
         if i is not None:
             ev[i][1].record(stream)
         if gathered is not None:
-            dist.all_gather_into_tensor(gathered, out)
+            if host_coll:
+                g = torch.empty(world * n * rec_bytes, dtype=torch.uint8)
+                dist.all_gather_into_tensor(g, out.cpu())
+                gathered.copy_(g)
+            else:
+                dist.all_gather_into_tensor(gathered, out)
 
     for _ in range(args.warmup):
         step()
@@ -123,7 +143,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
     if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if host_coll else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     ms_per_step = 1e3 * elapsed / args.steps
@@ -137,30 +157,31 @@ def main():
     epa_iters = (recs["diag"] >> 8) & 0xFF
     epa_mean = float(epa_iters[recs["collision"] != 0].mean()) if hit_rate > 0 else 0.0
 
-    bpq = algorithmic_bytes_per_query(args.nverts, args.nverts, 4, rec_bytes)
+    bpq = algorithmic_bytes_per_query(float(pool.hull_cnt.sum()) / n, 4, rec_bytes)
     achieved = n * bpq / (kern_ms * 1e-3) / 1e9
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
-            key = f"{args.precision}_{args.nverts}_{n}"
+            key = f"{args.precision}_{args.config}_{n}"
             if key in pj:
                 traffic = pj[key]["bytes_per_launch"]
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic,
-                "bytes_per_query": bpq, "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
-                "kernel": "gjkepa_tier_kernel (tiers 0-2 + memset, HIP events on the launch stream)"}
+                "bytes_per_query": round(bpq, 1), "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
+                "kernel": "gjk_kernel + epa_kernel tiers (one launch chain; HIP events on the launch stream)"}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "M queries/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.precision, "data": "synthetic",
-        "config": {"workload": f"C2: random {args.nverts}-vertex convex-hull pairs, fp32 vertex storage, "
-                               f"{args.precision} compute, version_={args.version}, TOL_FF_=1.0, r~U[0,{args.rmax}]",
+        "config": {"workload": f"{args.config}: {desc}, fp32 vertex storage, {args.precision} compute, "
+                               f"version_={args.version}, TOL_FF_=1.0, hull B offset r~U[0,{rmax}]",
+                   "hull_vertices": [nmin, nmax],
                    "pairs_per_gpu": n, "total_pairs": total_pairs, "seed": SEED,
                    "parallelism": f"shard{world}" + ("+allgather" if gathered is not None else ""),
                    "vert_storage": "f32", "record_bytes": rec_bytes},
@@ -192,7 +213,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # checker / CPU baseline only
-        m = min(args.cpu_sample, n)
+        m = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
         sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:m])
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
         oracle.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:256]),
@@ -202,7 +223,7 @@ def main():
         ct = time.perf_counter() - t
         result["cpu_baseline"] = {
             "value": round(m / ct / 1e6, 4), "unit": "M queries/s", "cores": threads, "kind": "port",
-            "sample": f"first {m} pairs of the same C2 batch, fp64 oracle restatement (oracle/gjkepa_oracle.c), "
+            "sample": f"first {m} pairs of the same {args.config} batch, fp64 oracle restatement (oracle/gjkepa_oracle.c), "
                       f"OpenMP dynamic over pairs, {ct:.2f} s wall",
         }
         if prec == gjkepa.PREC_F64:

@@ -43,13 +43,13 @@
 #define GJKEPA_E0_MINW 2
 #endif
 #ifndef GJKEPA_E1_G
-#define GJKEPA_E1_G 64
+#define GJKEPA_E1_G 32
 #endif
 #ifndef GJKEPA_E1_K
 #define GJKEPA_E1_K 1
 #endif
 #ifndef GJKEPA_E1_VCAP
-#define GJKEPA_E1_VCAP 64
+#define GJKEPA_E1_VCAP 72
 #endif
 #ifndef GJKEPA_E1_FCAP
 #define GJKEPA_E1_FCAP 128
