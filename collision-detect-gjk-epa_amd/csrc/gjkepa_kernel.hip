@@ -133,6 +133,40 @@ template <int S> DEV double xchg(double v) {
     return __builtin_bit_cast(double, (hi << 32) | lo);
 }
 
+// ---------------------------------------------------------------- diagnostic phase stamps
+// Built only with -DGJKEPA_DIAG_STAMPS (tools/build_variant.sh): wave time between consecutive
+// stamps is charged to the phase that ends at the stamp (s_memtime ticks, summed over waves).
+#ifdef GJKEPA_DIAG_STAMPS
+constexpr int kStamps = 32;
+__device__ unsigned long long g_stamps[kStamps];
+__shared__ unsigned long long s_stamp[kStamps + 1];
+DEV void stamp(int id) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    const uint64_t act = __ballot(1);
+    if ((uint64_t)lane_id() == (uint64_t)__builtin_ctzll(act)) { s_stamp[id] += t - s_stamp[kStamps]; s_stamp[kStamps] = t; }
+}
+DEV void stamp_begin() {
+    if (lane_id() == 0) {
+        for (int i = 0; i < kStamps; ++i) s_stamp[i] = 0;
+        s_stamp[kStamps] = __builtin_amdgcn_s_memtime();
+    }
+}
+DEV void stamp_end() {
+    if (lane_id() == 0)
+        for (int i = 0; i < kStamps; ++i) if (s_stamp[i]) atomicAdd(&g_stamps[i], s_stamp[i]);
+}
+#define GK_STAMP(id) stamp(id)
+#define GK_STAMP_BEGIN() stamp_begin()
+#define GK_STAMP_END() stamp_end()
+#else
+#define GK_STAMP(id) ((void)0)
+#define GK_STAMP_BEGIN() ((void)0)
+#define GK_STAMP_END() ((void)0)
+#endif
+enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
+       SE_LOAD = 10, SE_IT1, SE_DIR, SE_SUP, SE_VIS, SE_HOR, SE_CMP, SE_CONE, SE_TERM, SE_NEAR, SE_CONT, SE_TYPE,
+       SE_STORE, SE_ROUTE };
+
 template <int G> struct Grp {
     static constexpr int kSteps = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
     int lane, gl;
@@ -177,6 +211,16 @@ template <int S, int N, typename T> DEV void max_steps(T& v) {
         max_steps<S + 1, N>(v);
     }
 }
+// quad (4-lane) broadcast of lane j, DPP quad_perm [j,j,j,j]
+template <int J> DEV uint32_t qb32(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, J * 0x55, 0xF, 0xF, false); }
+template <int J> DEV double qbcast(double v) {
+    uint64_t u = __builtin_bit_cast(uint64_t, v);
+    return __builtin_bit_cast(double, ((uint64_t)qb32<J>((uint32_t)(u >> 32)) << 32) | qb32<J>((uint32_t)u));
+}
+template <int J> DEV float qbcast(float v) { return __builtin_bit_cast(float, qb32<J>(__builtin_bit_cast(uint32_t, v))); }
+DEV bool quad_all(bool b) { int x = b; x &= xchg<0>(x); x &= xchg<1>(x); return x != 0; }
+DEV bool quad_any(bool b) { int x = b; x |= xchg<0>(x); x |= xchg<1>(x); return x != 0; }
+
 // group-wide (value, index) argmax / argmin with lowest-index tie break; max
 template <int G, typename T> DEV void gargmax(T& v, int& i) { argmax_steps<0, Grp<G>::kSteps>(v, i); }
 template <int G, typename T> DEV void gargmin(T& v, int& i) { argmin_steps<0, Grp<G>::kSteps>(v, i); }
@@ -216,21 +260,32 @@ template <typename T, typename TH, int G, int K, int VC, int FC> struct Ctx {
 
 // ---------------------------------------------------------------- support mapping (:1030-1062)
 // indices: argmax_i d.a_i (first), argmax_j (-d).b_j (first); -dot(d,b) == dot(-d,b) bit for bit.
+// The group max of the values is reduced alone; the lowest index holding it is then found with
+// one ballot per register slot k (index k*G + lane: lower k first, then lower lane).
 CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
+    T ta[K], tb[K];
     T va = -Tol<T>::BIG, vb = -Tol<T>::BIG;
-    int xa = 0x7fffffff, xb = 0x7fffffff;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        int i = k * G + c.g.gl;
-        T ta = d.x * c.ax[k] + d.y * c.ay[k] + d.z * c.az[k];
-        if (i < c.na && ta > va) { va = ta; xa = i; }
-        T tb = -(d.x * c.bx[k] + d.y * c.by[k] + d.z * c.bz[k]);
-        if (i < c.nb && tb > vb) { vb = tb; xb = i; }
+        const int i = k * G + c.g.gl;
+        ta[k] = i < c.na ? d.x * c.ax[k] + d.y * c.ay[k] + d.z * c.az[k] : -Tol<T>::BIG;
+        tb[k] = i < c.nb ? -(d.x * c.bx[k] + d.y * c.by[k] + d.z * c.bz[k]) : -Tol<T>::BIG;
+        va = ta[k] > va ? ta[k] : va;
+        vb = tb[k] > vb ? tb[k] : vb;
     }
-    gargmax<G>(va, xa);
-    gargmax<G>(vb, xb);
-    ia = c.g.uni(xa == 0x7fffffff ? 0 : xa);
-    ib = c.g.uni(xb == 0x7fffffff ? 0 : xb);
+    va = gmax<G>(va);
+    vb = gmax<G>(vb);
+    const int sh = c.g.lane & ~(G - 1);
+    int xa = -1, xb = -1;
+#pragma unroll
+    for (int k = K - 1; k >= 0; --k) {
+        const uint64_t ma = (__ballot(ta[k] == va) >> sh) & (G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull));
+        const uint64_t mb = (__ballot(tb[k] == vb) >> sh) & (G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull));
+        if (ma) xa = k * G + (int)__builtin_ctzll(ma);
+        if (mb) xb = k * G + (int)__builtin_ctzll(mb);
+    }
+    ia = c.g.uni(xa < 0 ? 0 : xa);
+    ib = c.g.uni(xb < 0 ? 0 : xb);
 }
 CTX_T DEV V3<T> support(const CTX& c, V3<T> d) {
     int ia, ib;
@@ -268,6 +323,43 @@ template <typename T> DEV V3<T> centroid4(V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3
 }
 // candidate normal UTZVEC((a-b)x(b-c)) of the tetra faces idFc = [1,3,4],[1,2,4],[1,2,3],[2,3,4]
 template <typename T> DEV V3<T> face_nml(V3<T> a, V3<T> b, V3<T> cc) { return utzvec(cross(vsub(a, b), vsub(b, cc))); }
+
+// Lane-parallel tetrahedron faces: quad lane q = gl & 3 owns face q of idFc ([1,3,4], [1,2,4],
+// [1,2,3], [2,3,4]) with vertices (a, b, c) in idFc order.  Its raw normal UTZVEC((a-b)x(b-c)) is
+// computed once per simplex and serves both isPointInSimplex and the next update_simplex_GJK.
+template <typename T> DEV void quad_face(int q, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, V3<T>& a, V3<T>& b, V3<T>& cc) {
+    a = vsel(q == 3, s1, s0);
+    b = vsel(q == 0 || q == 3, s2, s1);
+    cc = vsel(q == 2, s2, s3);
+}
+template <typename T> DEV V3<T> quad_normal(int q, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& md) {
+    V3<T> a, b, cc;
+    quad_face(q, s0, s1, s2, s3, a, b, cc);
+    const V3<T> cr = cross(vsub(a, b), vsub(b, cc));
+    md = norm2(cr);
+    return md < Tol<T>::Z ? zero3<T>() : vdiv(cr, md);
+}
+// isPointInSimplex (:1217-1265) for P = origin from the quad's raw normals (same booleans as
+// origin_in_simplex: any boundary hit, else all four distances positive)
+template <typename T> DEV bool quad_inside(int q, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, V3<T> nq) {
+    const V3<T> M = centroid4(s0, s1, s2, s3);
+    const V3<T> ref = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
+    if (dot(nq, vsub(ref, M)) < T(0)) nq = vneg(nq);
+    const T d = dot(vsub(ref, zero3<T>()), nq);
+    bool bnd = false;
+    if (fabs(d) < Tol<T>::PT) {
+        V3<T> a, b, cc;
+        quad_face(q, s0, s1, s2, s3, a, b, cc);
+        bnd = inside_tri(a, b, cc, zero3<T>());
+    }
+    return quad_any(bnd) || quad_all(d > T(0));
+}
+// simplex coordinate j (point j/3, axis j%3) for the cycle history lanes
+template <typename T> DEV T simplex_coord(int j, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3) {
+    const int pt = j / 3, ax = j - 3 * (j / 3);
+    const V3<T> q = pt == 0 ? s0 : pt == 1 ? s1 : pt == 2 ? s2 : s3;
+    return ax == 0 ? q.x : ax == 1 ? q.y : q.z;
+}
 
 // isPointInSimplex (:1217-1265) for P = origin
 template <typename T> DEV bool origin_in_simplex(V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3) {
@@ -315,6 +407,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
     }
     nvis = c.g.uni(nvis);
     changed = nvis > 0;
+    GK_STAMP(SE_VIS);
     if (nvis == 0) return 0;
     int k = kexist;
     if (append) {
@@ -332,6 +425,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         }
     }
     __builtin_amdgcn_wave_barrier();
+    GK_STAMP(SE_VIS);
     // horizon edges: edge (u,w) of a visible face whose twin (w,u) is on no visible face
     int nh = 0;
     const int ne = 3 * nvis;
@@ -361,6 +455,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         nh += popc(m);
     }
     nh = c.g.uni(nh);
+    GK_STAMP(SE_HOR);
     const int nf2 = nf - nvis + nh;
     if (nh > FC || nf2 > FC) return ST_DEFER;
     if (save_eq && nf2 == nf) {
@@ -392,6 +487,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         base += popc(m);
         __builtin_amdgcn_wave_barrier();
     }
+    GK_STAMP(SE_CMP);
     // cone the horizon to k
     const V3<T> P = c.vert(k);
     bool bad = false;
@@ -408,6 +504,7 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         }
     }
     __builtin_amdgcn_wave_barrier();
+    GK_STAMP(SE_CONE);
     nf = nf2;
     if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
     return 0;
@@ -532,6 +629,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
             if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
             F1 = 4;
+            GK_STAMP(SE_IT1);
         } else {
             F1 = nf;                      // same faces, same order as last iteration's F2: reuse its MINLOC
             const int ml = ml_next;
@@ -559,7 +657,9 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             dt = dot(vsub(a1, M), dir);
         }
         if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+        GK_STAMP(iter == 1 ? SE_IT1 : SE_DIR);
         const V3<T> sp = support(c, dir);                          // :914
+        GK_STAMP(SE_SUP);
         const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
         int st;
         if (iter == 1) {
@@ -580,6 +680,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             if (two && gl == isp + 1) { q = sq; w = true; }
             if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
             __builtin_amdgcn_wave_barrier();
+            GK_STAMP(SE_IT1);
             st = hull_build(c, nv, nf, m);
         } else {
             if (two) {                    // net face count of two insertions unknown: save now
@@ -604,6 +705,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
         bool stop;                                                // :972-1015
         if (F1 == F2) stop = unchanged || sorted_equal(c, F1);   // unchanged hull: identical sorted lists
         else stop = F1 > F2;
+        GK_STAMP(SE_TERM);
         if (stop) { depth = minv2; normal = dir2; return 0; }
     }
 }
@@ -921,22 +1023,28 @@ CTX_T DEV V3<T> decode_pt(const CTX& c, uint32_t code) {
 }
 
 // update_simplex_GJK (:1070-1157) with vertex codes carried along
-CTX_T DEV void update_simplex_c(const CTX& c, V3<T>& s0, V3<T>& s1, V3<T>& s2, V3<T>& s3,
+// The four faces are evaluated on the quad lanes (raw normal nq of this lane's face q); the
+// first-index MAXLOC is a two-step quad butterfly that carries the winning normal along.
+CTX_T DEV void update_simplex_c(const CTX& c, V3<T> nq, V3<T>& s0, V3<T>& s1, V3<T>& s2, V3<T>& s3,
                                 uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
     const V3<T> M = centroid4(s0, s1, s2, s3), O = zero3<T>();
-    V3<T> n0 = face_nml(s0, s2, s3), n1 = face_nml(s0, s1, s3), n2 = face_nml(s0, s1, s2), n3 = face_nml(s1, s2, s3);
-    if (dot(n0, vsub(s0, M)) < T(0)) n0 = vneg(n0);
-    if (dot(n1, vsub(s0, M)) < T(0)) n1 = vneg(n1);
-    if (dot(n2, vsub(s0, M)) < T(0)) n2 = vneg(n2);
-    if (dot(n3, vsub(s1, M)) < T(0)) n3 = vneg(n3);
-    const T d0 = dot(vneg(n0), vsub(s0, O)), d1 = dot(vneg(n1), vsub(s0, O));
-    const T d2 = dot(vneg(n2), vsub(s0, O)), d3 = dot(vneg(n3), vsub(s1, O));
-    int k = 0;
-    T best = d0;
-    V3<T> dir = n0;
-    if (d1 > best) { best = d1; k = 1; dir = n1; }
-    if (d2 > best) { best = d2; k = 2; dir = n2; }
-    if (d3 > best) { best = d3; k = 3; dir = n3; }
+    const int q = c.g.gl & 3;
+    const V3<T> ref = q == 3 ? s1 : s0;
+    if (dot(nq, vsub(ref, M)) < T(0)) nq = vneg(nq);
+    T best = dot(vneg(nq), vsub(ref, O));
+    int k = q;
+    V3<T> dir = nq;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+        const T ob = st == 0 ? xchg<0>(best) : xchg<1>(best);
+        const int ok = st == 0 ? xchg<0>(k) : xchg<1>(k);
+        const V3<T> od = st == 0 ? vmk<T>(xchg<0>(dir.x), xchg<0>(dir.y), xchg<0>(dir.z))
+                                 : vmk<T>(xchg<1>(dir.x), xchg<1>(dir.y), xchg<1>(dir.z));
+        const bool take = ob > best || (ob == best && ok < k);
+        best = take ? ob : best;
+        k = take ? ok : k;
+        dir = vsel(take, od, dir);
+    }
     k = c.g.uni(k);
     uint32_t km;
     const V3<T> SM = support_pt(c, dir, km);
@@ -959,22 +1067,34 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     const int gl = c.g.gl;
     gjk_it = 0;
     {   // RoughCollisionDetection_SphericalEnvelope (:1165-1188)
-        T s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0, t2 = 0;
-        for (int i = 0; i < c.na; ++i) { s0 += (T)L.hx[0][i]; s1 += (T)L.hy[0][i]; s2 += (T)L.hz[0][i]; }
-        for (int i = 0; i < c.nb; ++i) { t0 += (T)L.hx[1][i]; t1 += (T)L.hy[1][i]; t2 += (T)L.hz[1][i]; }
-        const T dna = (T)c.na, dnb = (T)c.nb;
-        const V3<T> m1 = vmk<T>(s0 / dna, s1 / dna, s2 / dna), m2 = vmk<T>(t0 / dnb, t1 / dnb, t2 / dnb);
+        // the six sequential coordinate sums run on group lanes 0..5 (lane j: hull j/3, axis j%3)
+        T sum = 0;
+        if (gl < 6) {
+            const int h = gl / 3, ax = gl - 3 * (gl / 3);
+            const TH* col = ax == 0 ? L.hx[h] : ax == 1 ? L.hy[h] : L.hz[h];
+            const int n = h ? c.nb : c.na;
+            for (int i = 0; i < n; ++i) sum += (T)col[i];
+            sum = sum / (T)n;
+            L.u.g.l1[gl] = sum;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const V3<T> m1 = vmk<T>(L.u.g.l1[0], L.u.g.l1[1], L.u.g.l1[2]), m2 = vmk<T>(L.u.g.l1[3], L.u.g.l1[4], L.u.g.l1[5]);
+        __builtin_amdgcn_wave_barrier();
+        // max_i NORM2(p_i - m) = sqrt(max_i |p_i - m|^2): sqrt is monotone under correct rounding
         T r1 = -Tol<T>::BIG, r2 = -Tol<T>::BIG;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             int i = k * G + gl;
-            T ta = norm2(vsub(vmk<T>(c.ax[k], c.ay[k], c.az[k]), m1));
+            const V3<T> da = vsub(vmk<T>(c.ax[k], c.ay[k], c.az[k]), m1);
+            const T ta = da.x * da.x + da.y * da.y + da.z * da.z;
             if (i < c.na && ta > r1) r1 = ta;
-            T tb = norm2(vsub(vmk<T>(c.bx[k], c.by[k], c.bz[k]), m2));
+            const V3<T> db = vsub(vmk<T>(c.bx[k], c.by[k], c.bz[k]), m2);
+            const T tb = db.x * db.x + db.y * db.y + db.z * db.z;
             if (i < c.nb && tb > r2) r2 = tb;
         }
-        r1 = gmax<G>(r1);
-        r2 = gmax<G>(r2);
+        r1 = tsqrt(gmax<G>(r1));
+        r2 = tsqrt(gmax<G>(r2));
+        GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
     }
     // --- initial simplex (:82-170)
@@ -996,44 +1116,48 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     const T vd = dot(vsub(O, s2), dir);
     bool enter = false;
     if (c.g.unib(fabs(vd) < Tol<T>::PT) && c.g.unib(inside_tri(s0, s1, s2, O))) enter = true;
+    const int q = gl & 3;
+    V3<T> nq = zero3<T>();   // this quad lane's raw face normal of the current simplex
+    T mdq = 0;
     if (!enter) {
         if (c.g.unib(vd < T(0))) dir = vneg(dir);
         s3 = support_pt(c, dir, k3);
         const V3<T> n = uninml(s0, s1, s2);                         // DIST_PF_SIGN (:157)
         if (c.g.unib(is_zero_nml(n))) return GJKEPA_STATUS_DEGENERATE;
         if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return PH_MISS;
-        if (c.g.unib(origin_in_simplex(s0, s1, s2, s3))) enter = true;
+        nq = quad_normal(q, s0, s1, s2, s3, mdq);
+        if (c.g.unib(quad_inside(q, s0, s1, s2, s3, nq))) enter = true;
     }
+    GK_STAMP(SG_INIT);
     if (!enter) {
-        auto& H = L.u.g;
-        if (gl < 12) { H.l1[gl] = T(0); H.l2[gl] = T(0); }
+        // cycle history (:193-194): group lane j < 12 keeps coordinate j of last1 / last2
+        T h1 = 0, h2 = 0;
+        const uint64_t m12 = 0xFFFull;
+        const int sh = c.g.lane & ~(G - 1);
         for (int it = 1;; ++it) {                                        // :182-236
             gjk_it = it;
             if (it > 50) return PH_MISS;
-            // history: last2 = last1, last1 = simplex (:193-194); group lane j owns coordinate j
-            __builtin_amdgcn_wave_barrier();
-            if (gl < 12) {
-                const int pt = gl / 3, cc = gl - 3 * pt;
-                const V3<T> q = pt == 0 ? s0 : pt == 1 ? s1 : pt == 2 ? s2 : s3;
-                H.l2[gl] = H.l1[gl];
-                H.l1[gl] = cc == 0 ? q.x : cc == 1 ? q.y : q.z;
-            }
-            __builtin_amdgcn_wave_barrier();
-            update_simplex_c(c, s0, s1, s2, s3, k0, k1, k2, k3);
-            if (c.g.unib(norm2(cross(vsub(s1, s0), vsub(s2, s1))) < Tol<T>::PT)) return PH_MISS;   // :199-201
-            const V3<T> n = uninml(s0, s1, s2);
-            if (c.g.unib(is_zero_nml(n))) return GJKEPA_STATUS_DEGENERATE;
+            h2 = h1;
+            h1 = simplex_coord(gl < 12 ? gl : 0, s0, s1, s2, s3);
+            GK_STAMP(SG_CHK);
+            update_simplex_c(c, nq, s0, s1, s2, s3, k0, k1, k2, k3);
+            nq = quad_normal(q, s0, s1, s2, s3, mdq);
+            GK_STAMP(SG_UPD);
+            // :199-201 NORM2((s2-s1)x(s3-s2)) is face [1,2,3]'s |cross| (operands negated: same bits)
+            if (c.g.unib(qbcast<2>(mdq) < Tol<T>::PT)) return PH_MISS;
+            // :203 UNINML(s1,s2,s3) is then face [1,2,3]'s normal (|cross| >= 1e-8: never the zero case)
+            const V3<T> n = vmk<T>(qbcast<2>(nq.x), qbcast<2>(nq.y), qbcast<2>(nq.z));
             if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return PH_MISS;         // :203-206
-            if (c.g.unib(origin_in_simplex(s0, s1, s2, s3))) break;                       // :210-216
-            const V3<T> l10 = vmk<T>(H.l1[0], H.l1[1], H.l1[2]), l11 = vmk<T>(H.l1[3], H.l1[4], H.l1[5]);
-            const V3<T> l12 = vmk<T>(H.l1[6], H.l1[7], H.l1[8]), l13 = vmk<T>(H.l1[9], H.l1[10], H.l1[11]);
-            const V3<T> l20 = vmk<T>(H.l2[0], H.l2[1], H.l2[2]), l21 = vmk<T>(H.l2[3], H.l2[4], H.l2[5]);
-            const V3<T> l22 = vmk<T>(H.l2[6], H.l2[7], H.l2[8]), l23 = vmk<T>(H.l2[9], H.l2[10], H.l2[11]);
-            const bool over = (allclose8(s0, l10) || allclose8(s0, l20)) && (allclose8(s1, l11) || allclose8(s1, l21)) &&
-                              (allclose8(s2, l12) || allclose8(s2, l22)) && (allclose8(s3, l13) || allclose8(s3, l23));
-            if (c.g.unib(over)) return PH_MISS;                                           // :219-234
+            if (c.g.unib(quad_inside(q, s0, s1, s2, s3, nq))) break;                      // :210-216
+            const T cur = simplex_coord(gl < 12 ? gl : 0, s0, s1, s2, s3);               // :219-234
+            const uint32_t e1 = (uint32_t)((__ballot(fabs(cur - h1) < Tol<T>::PT) >> sh) & m12);
+            const uint32_t e2 = (uint32_t)((__ballot(fabs(cur - h2) < Tol<T>::PT) >> sh) & m12);
+            bool over = true;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) over = over && (((e1 >> (3 * p)) & 7u) == 7u || ((e2 >> (3 * p)) & 7u) == 7u);
+            if (c.g.unib(over)) return PH_MISS;
         }
-        __builtin_amdgcn_wave_barrier();
+        GK_STAMP(SG_CHK);
     }
     kc[0] = k0; kc[1] = k1; kc[2] = k2; kc[3] = k3;
     return PH_HIT;
@@ -1057,14 +1181,18 @@ CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, int version, T tol_ff, T* o1
     return -1;
 #endif
     int ia, ib;
+    GK_STAMP(SE_TERM);
     support_idx(c, n, ia, ib);                                           // get_nearest_points (:326, :813-855)
+    GK_STAMP(SE_NEAR);
     V3<T> pt = zero3<T>();
     if (version == 1) st = contact_v1(c, n, pt);                          // :329-340
     else if (version == 2) st = contact_v2(c, n, pt);
     else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; }
     else st = GJKEPA_STATUS_BAD_VERSION;
+    GK_STAMP(SE_CONT);
     if (st) return st;
     const int type = collision_type(c, n, tol_ff);                        // :343
+    GK_STAMP(SE_TYPE);
     const V3<T> q1 = c.A(ia), q2 = c.B(ib);
     o13[0] = depth;
     o13[1] = n.x; o13[2] = n.y; o13[3] = n.z;
@@ -1163,7 +1291,9 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
+    GK_STAMP_BEGIN();
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+        GK_STAMP(SG_ROUTE);
         Ctx<T, TIn, G, K, 4, 4> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
@@ -1178,13 +1308,16 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         } else {
             c.na = na;
             c.nb = nb;
-            if (load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb])) {
+            const bool bad_in = load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+            GK_STAMP(SG_LOAD);
+            if (bad_in) {
                 store_record<T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
             } else {
                 uint32_t kc[4];
                 int gjk_it = 0;
                 const int r = gjk_phase(c, kc, gjk_it);
                 __builtin_amdgcn_wave_barrier();
+                GK_STAMP(SG_CHK);
                 if (r == PH_HIT) {
                     if (gl < 5) {
                         const uint32_t word = gl == 0 ? kc[0] : gl == 1 ? kc[1] : gl == 2 ? kc[2] : gl == 3 ? kc[3] : (uint32_t)gjk_it;
@@ -1200,7 +1333,10 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         }
         if (gl == 0) a.route[pair] = next;
         __builtin_amdgcn_wave_barrier();
+        GK_STAMP(SG_STORE);
     });
+    GK_STAMP(SG_ROUTE);
+    GK_STAMP_END();
 }
 
 // EPA kernel: EPA + contact features for the pairs routed to this tier.  A polytope that outgrows
@@ -1213,7 +1349,9 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
+    GK_STAMP_BEGIN();
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+        GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, VC, FC> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
@@ -1227,6 +1365,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
         uint32_t de = 0;
+        GK_STAMP(SE_LOAD);
         const int r = epa_phase(c, kc, a.version, (T)a.tol_ff, o13, de);
         __builtin_amdgcn_wave_barrier();
         uint8_t next = 0;
@@ -1245,7 +1384,10 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
         }
         if (gl == 0) a.route[pair] = next;
         __builtin_amdgcn_wave_barrier();
+        GK_STAMP(SE_STORE);
     });
+    GK_STAMP(SE_ROUTE);
+    GK_STAMP_END();
 }
 
 }  // namespace gk
@@ -1302,6 +1444,18 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
 }
 
 }  // namespace
+
+#ifdef GJKEPA_DIAG_STAMPS
+// diagnostic build only: read (and optionally clear) the phase stamp totals
+extern "C" int gjkepa_diag_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gk::g_stamps), sizeof(gk::g_stamps)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[gk::kStamps] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gk::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return gk::kStamps;
+}
+#endif
 
 hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s) {
     if (vert_dtype == GJKEPA_DTYPE_F32)
