@@ -1,8 +1,10 @@
 // gjkepa_kernel.h — host-side interface of the GJK and EPA kernels (internal, not the C-ABI).
 //
-// Two phases, each in tiers.  GJK tier 0 takes every pair (hulls up to G0*K0 vertices; larger
+// Three phases, each in tiers.  GJK tier 0 takes every pair (hulls up to G0*K0 vertices; larger
 // hulls go to GJK tier 1).  Misses and errors are final after GJK; each hit is routed to the
-// smallest EPA tier whose hull capacity holds it.  An EPA tier that runs out of polytope capacity
+// smallest EPA tier whose hull capacity holds it.  EPA parks depth and normal in the pair's
+// record and routes it to the contact tier for its hull size (nearest points, contact point,
+// contact type), which writes the final record.  An EPA tier that runs out of polytope capacity
 // (VCAP vertices / FCAP faces) routes the pair to the next EPA tier, which
 // recomputes it from the same GJK simplex; the last EPA tier holds the worst case the reference
 // allows (6 + 2*99 EPA points, 2V-4 faces), so it never defers.  Which tier answered never
@@ -15,13 +17,13 @@
 
 // GJK tiers: G lanes per pair (64/G pairs per wave), K vertices per lane per hull (hull <= G*K)
 #ifndef GJKEPA_G0_G
-#define GJKEPA_G0_G 16
+#define GJKEPA_G0_G 4           // 16 pairs per wave: GJK is VALU-bound on group-uniform work
 #endif
 #ifndef GJKEPA_G0_K
-#define GJKEPA_G0_K 2
+#define GJKEPA_G0_K 8
 #endif
 #ifndef GJKEPA_G0_MINW
-#define GJKEPA_G0_MINW 3        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
+#define GJKEPA_G0_MINW 2        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
 #endif
 #define GJKEPA_G1_G 64
 #define GJKEPA_G1_K 4
@@ -87,13 +89,30 @@
 #ifndef GJKEPA_E3_MINW
 #define GJKEPA_E3_MINW 1
 #endif
+// contact-feature tiers (nearest points, contact point, contact type): G, K as above
+#ifndef GJKEPA_C0_G
+#define GJKEPA_C0_G 16
+#endif
+#ifndef GJKEPA_C0_K
+#define GJKEPA_C0_K 2
+#endif
+#ifndef GJKEPA_C0_MINW
+#define GJKEPA_C0_MINW 2
+#endif
+#define GJKEPA_C1_G 64
+#define GJKEPA_C1_K 4
+#define GJKEPA_C1_MINW 1
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 4
+#define GJKEPA_CONTACT_TIERS 2
 
+// workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair
+#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (8 launches used)
 // route byte per pair (workspace): which kernel owns the pair next
 #define GJKEPA_ROUTE_DONE 0
 #define GJKEPA_ROUTE_GJK1 1
 #define GJKEPA_ROUTE_EPA0 0x10      // + EPA tier
+#define GJKEPA_ROUTE_CT0 0x20       // + contact tier
 
 struct gjkepa_gjk_args {
     const void* verts;
@@ -103,6 +122,8 @@ struct gjkepa_gjk_args {
     int64_t n_pairs;
     uint8_t* route;             // [n_pairs]
     int route_code;             // pairs this launch serves: -1 = all (tier 0), else route code
+    uint32_t* ctr;              // this launch's chunk counter (zero at launch)
+    int claim;                  // 64-pair chunks taken per counter increment
     void* out;                  // contact records (hits: simplex codes parked in their slot)
     int grid;                   // <= 0: occupancy x CUs
     int num_cus;
@@ -119,6 +140,8 @@ struct gjkepa_epa_args {
     uint8_t* route;
     int route_code;             // GJKEPA_ROUTE_EPA0 + tier
     int next_code;              // route code for polytope overflow; -1 on the last tier
+    uint32_t* ctr;              // this launch's chunk counter (zero at launch)
+    int claim;                  // 64-pair chunks taken per counter increment
     void* out;
     int grid;
     int num_cus;
@@ -126,3 +149,5 @@ struct gjkepa_epa_args {
 
 hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s);
 hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
+// contact tiers take the same argument block (route_code = GJKEPA_ROUTE_CT0 + tier; next_code unused)
+hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);

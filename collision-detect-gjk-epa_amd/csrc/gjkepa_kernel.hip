@@ -158,6 +158,10 @@ DEV void stamp_end() {
 #define GK_STAMP(id) stamp(id)
 #define GK_STAMP_BEGIN() stamp_begin()
 #define GK_STAMP_END() stamp_end()
+#elif defined(GJKEPA_DIAG_MARKERS)   // ISA region markers for static instruction counts (tools/isa_regions.py)
+#define GK_STAMP(id) asm volatile("; GKMARK %0" ::"n"(id))
+#define GK_STAMP_BEGIN() ((void)0)
+#define GK_STAMP_END() ((void)0)
 #else
 #define GK_STAMP(id) ((void)0)
 #define GK_STAMP_BEGIN() ((void)0)
@@ -225,19 +229,35 @@ DEV bool quad_any(bool b) { int x = b; x |= xchg<0>(x); x |= xchg<1>(x); return 
 template <int G, typename T> DEV void gargmax(T& v, int& i) { argmax_steps<0, Grp<G>::kSteps>(v, i); }
 template <int G, typename T> DEV void gargmin(T& v, int& i) { argmin_steps<0, Grp<G>::kSteps>(v, i); }
 template <int G, typename T> DEV T gmax(T v) { max_steps<0, Grp<G>::kSteps>(v); return v; }
+template <int S, int N, typename T> DEV void min_steps(T& v) {
+    if constexpr (S < N) {
+        T ov = xchg<S>(v);
+        v = ov < v ? ov : v;
+        min_steps<S + 1, N>(v);
+    }
+}
+template <int G, typename T> DEV T gmin(T v) { min_steps<0, Grp<G>::kSteps>(v); return v; }
 
 // ---------------------------------------------------------------- per-group LDS image
 template <typename T, typename TH, int G, int K, int VC, int FC> struct Lds {
     static constexpr int NH = G * K;
     TH hx[2][NH], hy[2][NH], hz[2][NH];  // hull A (0) / B (1) vertices, storage precision
     union U {
-        struct E {                       // EPA polytope
-            T vx[VC], vy[VC], vz[VC];
-            T fnx[FC], fny[FC], fnz[FC]; // face unit normal UNINML(stored order), outward
-            T fd[FC];                    // |DIST_PF_SIGN(O, face)|
-            T dsv[FC];                   // previous iteration's distances (termination test)
-            uint32_t fv[FC];             // vertex ids v0 | v1<<8 | v2<<16
-            union X { struct H { uint32_t visf[FC]; uint32_t hor[FC]; } h; T srt[FC]; } x;
+        struct E {                       // EPA polytope (faces themselves are in registers)
+            T vx[VC], vy[VC], vz[VC];    // vertices by id
+            T dsv[FC];                   // saved face distances by slot (termination test), NaN = none
+            T best[3];                   // MINLOC face broadcast: normal, first vertex id
+            uint32_t bestv;
+            union X {
+                struct H {                                                                 // hull_add lists
+                    uint64_t visl[FC];                       // visible faces: ids | key << 32
+                    uint32_t horu[FC], hork[FC];             // horizon edges: u | w << 8, new face key
+                    T sn[G][4];                              // new faces of one round: normal, |distance|
+                    uint32_t sv[G], sk[G];                   //   ids, key
+                } h;
+                struct S { T cur[FC]; T srt[FC]; } s;                                     // sorted_equal
+                struct O { uint32_t key[FC]; uint32_t ord[FC]; } o;                       // centroid order
+            } x;
         } e;
         struct Gh { T l1[12], l2[12]; } g;   // GJK simplex history (:193-194)
         struct C { T sx[NH], sy[NH], sz[NH], pol[NH]; uint32_t ord[NH]; } c;   // contact features
@@ -253,7 +273,6 @@ template <typename T, typename TH, int G, int K, int VC, int FC> struct Ctx {
     DEV V3<T> A(int i) const { return vmk<T>((T)L.hx[0][i], (T)L.hy[0][i], (T)L.hz[0][i]); }
     DEV V3<T> B(int i) const { return vmk<T>((T)L.hx[1][i], (T)L.hy[1][i], (T)L.hz[1][i]); }
     DEV V3<T> vert(int i) const { return vmk<T>(L.u.e.vx[i], L.u.e.vy[i], L.u.e.vz[i]); }
-    DEV V3<T> fn(int f) const { return vmk<T>(L.u.e.fnx[f], L.u.e.fny[f], L.u.e.fnz[f]); }
 };
 #define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC>
 #define CTX Ctx<T, TH, G, K, VC, FC>
@@ -377,30 +396,44 @@ template <typename T> DEV bool origin_in_simplex(V3<T> s0, V3<T> s1, V3<T> s2, V
     return d0 > T(0) && d1 > T(0) && d2 > T(0) && d3 > T(0);
 }
 // ---------------------------------------------------------------- EPA polytope (re-supplied hull)
-CTX_T DEV void write_face(CTX& c, int f, int a, int b, int d, V3<T> n, T dist) {
-    auto& E = c.L.u.e;
-    E.fv[f] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)d << 16);
-    E.fnx[f] = n.x; E.fny[f] = n.y; E.fnz[f] = n.z;
-    E.fd[f] = dist;
-}
+// Faces live in registers: face slot f = r*G + lane is row r of group lane f % G (R = FC/G rows).
+// A face holds its unit normal UNINML (stored order, outward), |DIST_PF_SIGN(O, face)|, its
+// vertex ids and a creation key; vertex coordinates are read from the LDS vertex list.  The reference's face list order
+// (survivors in order, then new faces by (visible face, edge)) is the order of creation, so the
+// key stands in for the list position: MINLOC's "first index" is the lowest key, and faces never
+// move.  New faces take the lowest free slots; holes are reused.
+constexpr uint32_t kEmpty = 0x80000000u;
 
-// Add point p (vertex id k; appended at nv when `append`) — visible faces (signed distance >
-// HULL) removed, horizon coned to k.  Order: survivors, then new faces by (visible face, edge).
-// `changed` reports whether the hull changed; with `save_eq` the current distances are copied to
-// dsv[] when the face count will not change (the only case the termination test reads them).
-CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexist, bool& changed, bool save_eq) {
+template <typename T, int R> struct Faces {
+    T nx[R], ny[R], nz[R];     // unit normal
+    T d[R];                    // |plane distance of the origin|
+    uint32_t fv[R];            // v0 | v1 << 8 | v2 << 16, kEmpty = free slot
+    uint32_t key[R];           // creation order
+};
+#define FACES_T Faces<T, (FC + G - 1) / G>
+
+template <typename T> DEV T qnan() { return __builtin_nan(""); }
+
+// Add point p (vertex id k; appended at nv when `append`): faces it sees (signed distance >
+// HULL) are removed and the horizon is coned to k.  `changed` reports whether the hull changed;
+// with `save_eq` the current distances are saved to dsv[] when the face count will not change
+// (the only case the termination test reads them).
+CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3<T> p, bool append, int kexist,
+                       bool& changed, bool save_eq) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
     uint64_t vm[R];
+    bool live[R];            // some face of this row is valid somewhere in the wave
     int nvis = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int f = r * G + gl;
+        const bool valid = !(F.fv[r] & kEmpty);
         bool vis = false;
-        if (f < nf) {
-            int a = (int)(E.fv[f] & 0xffu);
-            vis = dot(vsub(p, c.vert(a)), c.fn(f)) > Tol<T>::HULL;
+        live[r] = __ballot(valid) != 0;
+        if (live[r]) {
+            const V3<T> a = c.vert(valid ? (int)(F.fv[r] & 0xffu) : 0), n = vmk<T>(F.nx[r], F.ny[r], F.nz[r]);
+            vis = valid && dot(vsub(p, a), n) > Tol<T>::HULL;
         }
         vm[r] = c.g.ballot(vis);
         nvis += popc(vm[r]);
@@ -416,41 +449,49 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
         if (gl == 0) { E.vx[k] = p.x; E.vy[k] = p.y; E.vz[k] = p.z; }
         nv = nv + 1;
     }
-    {   // visible face list, in face order
+    {   // visible faces (ids, key) in slot order
         int base = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (c.g.bit(vm[r])) E.x.h.visf[base + mbcnt(vm[r])] = (uint32_t)(r * G + gl);
+            if (!live[r]) continue;
+            if (c.g.bit(vm[r])) E.x.h.visl[base + mbcnt(vm[r])] = (uint64_t)F.fv[r] | ((uint64_t)F.key[r] << 32);
             base += popc(vm[r]);
         }
     }
     __builtin_amdgcn_wave_barrier();
     GK_STAMP(SE_VIS);
-    // horizon edges: edge (u,w) of a visible face whose twin (w,u) is on no visible face
+    // horizon edges: edge s = (v_s, v_s+1) of a visible face whose twin (w,u) is on no visible
+    // face.  Its new face's key follows the reference order: (rank of the face among the visible
+    // ones by key, s).
     int nh = 0;
     const int ne = 3 * nvis;
     for (int e0 = 0; e0 < ne; e0 += G) {
-        int e = e0 + gl;
+        const int e = e0 + gl;
         bool hz = false;
-        uint32_t uw = 0;
+        uint32_t uw = 0, nkey = 0;
         if (e < ne) {
-            int fi = e / 3, s = e - 3 * fi;
-            uint32_t fv = E.fv[E.x.h.visf[fi]];
-            uint32_t u = (fv >> (8 * s)) & 0xffu;
-            uint32_t w = (fv >> (8 * (s == 2 ? 0 : s + 1))) & 0xffu;
+            const int fi = e / 3, s = e - 3 * fi;
+            const uint64_t me = E.x.h.visl[fi];
+            const uint32_t fv = (uint32_t)me, kk = (uint32_t)(me >> 32);
+            const uint32_t u = (fv >> (8 * s)) & 0xffu;
+            const uint32_t w = (fv >> (8 * (s == 2 ? 0 : s + 1))) & 0xffu;
             bool twin = false;
-            for (int j = 0; j < nvis && !twin; ++j) {
-                uint32_t q = E.fv[E.x.h.visf[j]];
-                uint32_t q0 = q & 0xffu, q1 = (q >> 8) & 0xffu, q2 = (q >> 16) & 0xffu;
-                twin = (q0 == w && q1 == u) || (q1 == w && q2 == u) || (q2 == w && q0 == u);
+            int rank = 0;
+            for (int j = 0; j < nvis; ++j) {
+                const uint64_t qj = E.x.h.visl[j];
+                const uint32_t q = (uint32_t)qj;
+                const uint32_t q0 = q & 0xffu, q1 = (q >> 8) & 0xffu, q2 = (q >> 16) & 0xffu;
+                twin = twin || (q0 == w && q1 == u) || (q1 == w && q2 == u) || (q2 == w && q0 == u);
+                rank += (uint32_t)(qj >> 32) < kk;
             }
             hz = !twin;
             uw = u | (w << 8);
+            nkey = kbase + 3u * (uint32_t)rank + (uint32_t)s;
         }
-        uint64_t m = c.g.ballot(hz);
+        const uint64_t m = c.g.ballot(hz);
         if (hz) {
-            int pos = nh + mbcnt(m);
-            if (pos < FC) E.x.h.hor[pos] = uw;
+            const int pos = nh + mbcnt(m);
+            if (pos < FC) { E.x.h.horu[pos] = uw; E.x.h.hork[pos] = nkey; }
         }
         nh += popc(m);
     }
@@ -458,52 +499,67 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
     GK_STAMP(SE_HOR);
     const int nf2 = nf - nvis + nh;
     if (nh > FC || nf2 > FC) return ST_DEFER;
+    kbase += 3u * (uint32_t)nvis;
     if (save_eq && nf2 == nf) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            int f = r * G + gl;
-            if (f < nf) E.dsv[f] = E.fd[f];
-        }
-    }
-    // compact surviving faces (order preserved; in place is safe: new index <= old index).
-    // Rows before the first visible face do not move.
-    int base = 0;
-    bool moving = false;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        moving = moving || vm[r] != 0;
-        if (!moving) { base += G; continue; }
-        int f = r * G + gl;
-        bool keep = f < nf && !c.g.bit(vm[r]);
-        uint32_t fv = 0;
-        T nx = 0, ny = 0, nz = 0, d = 0;
-        if (keep) { fv = E.fv[f]; nx = E.fnx[f]; ny = E.fny[f]; nz = E.fnz[f]; d = E.fd[f]; }
-        uint64_t m = c.g.ballot(keep);
-        __builtin_amdgcn_wave_barrier();
-        if (keep) {
-            int pos = base + mbcnt(m);
-            if (pos != f) { E.fv[pos] = fv; E.fnx[pos] = nx; E.fny[pos] = ny; E.fnz[pos] = nz; E.fd[pos] = d; }
-        }
-        base += popc(m);
-        __builtin_amdgcn_wave_barrier();
-    }
-    GK_STAMP(SE_CMP);
-    // cone the horizon to k
-    const V3<T> P = c.vert(k);
-    bool bad = false;
-    for (int h0 = 0; h0 < nh; h0 += G) {
-        int h = h0 + gl;
-        if (h < nh) {
-            uint32_t uw = E.x.h.hor[h];
-            int u = (int)(uw & 0xffu), w = (int)((uw >> 8) & 0xffu);
-            V3<T> U = c.vert(u), W = c.vert(w);
-            V3<T> n = uninml(U, W, P);
-            if (is_zero_nml(n)) bad = true;
-            T d = fabs(dot(vsub(zero3<T>(), U), n));
-            write_face(c, base + h, u, w, k, n, d);
+            const int f = r * G + gl;
+            if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
         }
     }
     __builtin_amdgcn_wave_barrier();
+    GK_STAMP(SE_CMP);
+    // New faces (horizon edge h coned to k) are built G at a time on group lane h % G and staged
+    // in LDS; the visible faces go and the new faces take the first nh free slots in slot order.
+    const V3<T> P = c.vert(k);
+    bool bad = false;
+    int fr[R];
+    {
+        int fbase = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!live[r] && (r + 1) * G <= FC) {   // every slot of the row is free
+                fr[r] = fbase + gl;
+                fbase += G;
+                continue;
+            }
+            const bool vis = c.g.bit(vm[r]);
+            const bool fre = ((F.fv[r] & kEmpty) || vis) && (r * G + gl < FC);
+            const uint64_t fm = c.g.ballot(fre);
+            fr[r] = fre ? fbase + mbcnt(fm) : 0x7fffffff;
+            fbase += popc(fm);
+            if (vis) F.fv[r] = kEmpty;
+        }
+    }
+    for (int h0 = 0; h0 < nh; h0 += G) {
+        const int h = h0 + gl;
+        if (h < nh) {
+            const uint32_t uw = E.x.h.horu[h];
+            const int u = (int)(uw & 0xffu), w = (int)((uw >> 8) & 0xffu);
+            const V3<T> U = c.vert(u), W = c.vert(w);
+            const V3<T> n = uninml(U, W, P);
+            bad = bad || is_zero_nml(n);
+            E.x.h.sn[gl][0] = n.x; E.x.h.sn[gl][1] = n.y; E.x.h.sn[gl][2] = n.z;
+            E.x.h.sn[gl][3] = fabs(dot(vsub(zero3<T>(), U), n));
+            E.x.h.sv[gl] = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
+            E.x.h.sk[gl] = E.x.h.hork[h];
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = fr[r] - h0;
+            const bool tgt = j >= 0 && j < G && fr[r] < nh;
+            if (__ballot(tgt)) {
+                if (tgt) {
+                    F.nx[r] = E.x.h.sn[j][0]; F.ny[r] = E.x.h.sn[j][1]; F.nz[r] = E.x.h.sn[j][2];
+                    F.d[r] = E.x.h.sn[j][3];
+                    F.fv[r] = E.x.h.sv[j];
+                    F.key[r] = E.x.h.sk[j];
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
     GK_STAMP(SE_CONE);
     nf = nf2;
     if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
@@ -512,8 +568,9 @@ CTX_T DEV int hull_add(CTX& c, int& nv, int& nf, V3<T> p, bool append, int kexis
 
 // Hull of <= 6 points from scratch (EPA iteration 1): the points are vertex ids 0..m-1 of the
 // polytope.  First non-degenerate tetrahedron in list order, faces in the seed pattern of
-// :279-293 wound outward, then the remaining points in order.
-CTX_T DEV int hull_build(CTX& c, int& nv, int& nf, int m) {
+// :279-293 wound outward (slots / keys 0..3), then the remaining points in order.
+CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, int m) {
+    constexpr int R = (FC + G - 1) / G;
     nv = m;
     nf = 0;
     const V3<T> P0 = c.vert(0);
@@ -533,9 +590,11 @@ CTX_T DEV int hull_build(CTX& c, int& nv, int& nf, int m) {
     if (i3 < 0) return GJKEPA_STATUS_DEGENERATE;
     const V3<T> P3 = c.vert(i3);
     const V3<T> cen = centroid4(P0, P1, P2, P3);
-    // seed faces over tetra slots (0,1,2),(0,2,3),(0,1,3),(1,2,3); group lane f writes face f
+    // seed faces over tetra slots (0,1,2),(0,2,3),(0,1,3),(1,2,3); group lane f owns face f
     const int gl = c.g.gl;
     bool bad = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) F.fv[r] = kEmpty;
     if (gl < 4) {
         int a = gl == 3 ? i1 : 0, b = (gl == 0 || gl == 2) ? i1 : i2, d = gl == 0 ? i2 : i3;
         V3<T> Pa = vsel(gl == 3, P1, P0);
@@ -545,168 +604,237 @@ CTX_T DEV int hull_build(CTX& c, int& nv, int& nf, int m) {
         if (dot(n0, vsub(Pa, cen)) < T(0)) { int s = b; b = d; d = s; V3<T> q = Pb; Pb = Pd; Pd = q; }
         const V3<T> n = uninml(Pa, Pb, Pd);
         bad = is_zero_nml(n);
-        const T dist = fabs(dot(vsub(zero3<T>(), Pa), n));
-        write_face(c, gl, a, b, d, n, dist);
+        F.nx[0] = n.x; F.ny[0] = n.y; F.nz[0] = n.z;
+        F.d[0] = fabs(dot(vsub(zero3<T>(), Pa), n));
+        F.fv[0] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)d << 16);
+        F.key[0] = (uint32_t)gl;
     }
-    __builtin_amdgcn_wave_barrier();
     if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
     nf = 4;
+    kbase = 4;
     for (int j = 1; j < m; ++j) {
         if (j == i1 || j == i2 || j == i3) continue;
         bool ch;
-        int st = hull_add(c, nv, nf, c.vert(j), false, j, ch, false);
+        int st = hull_add(c, F, kbase, nv, nf, c.vert(j), false, j, ch, false);
         if (st) return st;
     }
     return 0;
 }
 
-// first-index argmin of fd[0..nf)
-CTX_T DEV int face_argmin(CTX& c, int nf) {
+// MINLOC of the face distances (first in list order = lowest key): value-only group min, then
+// the key breaks a tie between lanes.  The winner's normal, first vertex and distance are
+// broadcast through the group's LDS slot.
+CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, V3<T>& a) {
     constexpr int R = (FC + G - 1) / G;
+    auto& E = c.L.u.e;
     T v = Tol<T>::BIG;
-    int idx = 0x7fffffff;
+    uint32_t kk = 0xFFFFFFFFu;
+    int rr = -1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int f = r * G + c.g.gl;
-        if (f < nf) { T d = c.L.u.e.fd[f]; if (idx == 0x7fffffff || d < v) { v = d; idx = f; } }
+        const bool valid = !(F.fv[r] & kEmpty);
+        if (!__ballot(valid)) continue;
+        if (valid && (F.d[r] < v || (F.d[r] == v && F.key[r] < kk))) { v = F.d[r]; kk = F.key[r]; rr = r; }
     }
-    gargmin<G>(v, idx);
-    return c.g.uni(idx == 0x7fffffff ? 0 : idx);
+    const T vmin = gmin<G>(v);
+    const bool tie = rr >= 0 && v == vmin;
+    uint64_t m = c.g.ballot(tie);
+    if (c.g.unib(popc(m) > 1)) {
+        const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
+        m = c.g.ballot(tie && kk == kmin);
+    }
+    if (c.g.bit(m)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (rr == r) {
+                E.best[0] = F.nx[r]; E.best[1] = F.ny[r]; E.best[2] = F.nz[r];
+                E.bestv = F.fv[r] & 0xffu;
+            }
+    }
+    __builtin_amdgcn_wave_barrier();
+    dmin = vmin;
+    n = vmk<T>(E.best[0], E.best[1], E.best[2]);
+    a = c.vert((int)E.bestv);
+    __builtin_amdgcn_wave_barrier();
 }
 
-// ALL(|sort(d1) - sort(d2)| < 1e-8), d1 = dsv[0..n), d2 = fd[0..n)  (:972-1004)
-CTX_T DEV bool sorted_equal(CTX& c, int n) {
+// ALL(|sort(d1) - sort(d2)| < 1e-8), d1 = dsv[] (saved, NaN = no face), d2 = the current faces
+// (:972-1004).  Both lists hold n values.
+CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F) {
+    constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
-    for (int i0 = 0; i0 < n; i0 += G) {
-        int i = i0 + c.g.gl;
-        if (i < n) {
-            T x = E.fd[i];
-            int r = 0;
-            for (int j = 0; j < n; ++j) { T y = E.fd[j]; r += (y < x) || (y == x && j < i); }
-            E.x.srt[r] = x;
+    const int gl = c.g.gl;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        if (f < FC) E.x.s.cur[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * G + gl;
+        if (i < FC) {
+            const T x = E.x.s.cur[i];
+            if (x == x) {
+                int rk = 0;
+                for (int j = 0; j < FC; ++j) { const T y = E.x.s.cur[j]; rk += (y < x) || (y == x && j < i); }
+                E.x.s.srt[rk] = x;
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();
     bool ok = true;
-    for (int i0 = 0; i0 < n; i0 += G) {
-        int i = i0 + c.g.gl;
-        if (i < n) {
-            T x = E.dsv[i];
-            int r = 0;
-            for (int j = 0; j < n; ++j) { T y = E.dsv[j]; r += (y < x) || (y == x && j < i); }
-            if (!(fabs(x - E.x.srt[r]) < Tol<T>::PT)) ok = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * G + gl;
+        if (i < FC) {
+            const T x = E.dsv[i];
+            if (x == x) {
+                int rk = 0;
+                for (int j = 0; j < FC; ++j) { const T y = E.dsv[j]; rk += (y < x) || (y == x && j < i); }
+                if (!(fabs(x - E.x.s.srt[rk]) < Tol<T>::PT)) ok = false;
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();
     return c.g.all(ok);
 }
 
-// EPA_solu loop (:274-323) + update_expandingPolytope_EPA (:863-1022)
+// SUM(polytope) / (3 F) over the face list in order (:905-908): faces sorted by key, then the
+// sequential sum over vertex slot j = 0..2 and face f (column-major polytope(F,3,3)).
+CTX_T DEV V3<T> polytope_centroid(CTX& c, const FACES_T& F, int nf) {
+    constexpr int R = (FC + G - 1) / G;
+    auto& E = c.L.u.e;
+    const int gl = c.g.gl;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        if (f < FC) E.x.o.key[f] = (F.fv[r] & kEmpty) ? 0xFFFFFFFFu : F.key[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        if (f < FC && !(F.fv[r] & kEmpty)) {
+            int rk = 0;
+            for (int j = 0; j < FC; ++j) rk += E.x.o.key[j] < F.key[r];
+            E.x.o.ord[rk] = F.fv[r];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    T sx = 0, sy = 0, sz = 0;
+    for (int j = 0; j < 3; ++j)
+        for (int f = 0; f < nf; ++f) {
+            const V3<T> q = c.vert((int)((E.x.o.ord[f] >> (8 * j)) & 0xffu));
+            sx += q.x; sy += q.y; sz += q.z;
+        }
+    __builtin_amdgcn_wave_barrier();
+    const T cnt = (T)(nf * 3);
+    return vmk<T>(sx / cnt, sy / cnt, sz / cnt);
+}
+
+// EPA_solu loop (:274-323) + update_expandingPolytope_EPA (:863-1022).  Iteration 1 (seed soup
+// and hull from scratch) is peeled so the GJK simplex is dead inside the loop.
 CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const V3<T> O = zero3<T>();
     const int gl = c.g.gl;
-    int nv = 0, ml_next = 0;
+    FACES_T F;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        F.fv[r] = kEmpty;
+        const int f = r * G + gl;
+        if (f < FC) E.dsv[f] = qnan<T>();
+    }
+    int nv = 0;
+    uint32_t kbase = 0;
     nf = 0;
-    for (int iter = 1;; ++iter) {
-        iters = iter;
-        if (iter > 99) return GJKEPA_STATUS_EPA_MAXITER;
-        bool unchanged = false;
-        int F1;
-        T minv;
-        V3<T> dir, a1;
-        if (iter == 1) {
-            // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN
-            const V3<T> f0 = uninml(s0, s1, s2), f1 = uninml(s0, s2, s3), f2 = uninml(s0, s1, s3), f3 = uninml(s1, s2, s3);
-            if (c.g.unib(is_zero_nml(f0) || is_zero_nml(f1) || is_zero_nml(f2) || is_zero_nml(f3)))
-                return GJKEPA_STATUS_DEGENERATE;
-            const T d0 = fabs(dot(vsub(O, s0), f0)), d1 = fabs(dot(vsub(O, s0), f1));
-            const T d2 = fabs(dot(vsub(O, s0), f2)), d3 = fabs(dot(vsub(O, s1), f3));
-            minv = d0; dir = f0; a1 = s0;
-            if (d1 < minv) { minv = d1; dir = f1; a1 = s0; }
-            if (d2 < minv) { minv = d2; dir = f2; a1 = s0; }
-            if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
-            if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
-            F1 = 4;
-            GK_STAMP(SE_IT1);
-        } else {
-            F1 = nf;                      // same faces, same order as last iteration's F2: reuse its MINLOC
-            const int ml = ml_next;
-            minv = E.fd[ml];
-            dir = c.fn(ml);
-            a1 = c.vert((int)(E.fv[ml] & 0xffu));
-        }
+    T minv = 0;
+    V3<T> dir = O, a1 = O;           // MINLOC face of the current polytope (normal, first vertex)
+    iters = 1;
+    {   // ---- iteration 1
+        // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN
+        const V3<T> f0 = uninml(s0, s1, s2), f1 = uninml(s0, s2, s3), f2 = uninml(s0, s1, s3), f3 = uninml(s1, s2, s3);
+        if (c.g.unib(is_zero_nml(f0) || is_zero_nml(f1) || is_zero_nml(f2) || is_zero_nml(f3)))
+            return GJKEPA_STATUS_DEGENERATE;
+        const T d0 = fabs(dot(vsub(O, s0), f0)), d1 = fabs(dot(vsub(O, s0), f1));
+        const T d2 = fabs(dot(vsub(O, s0), f2)), d3 = fabs(dot(vsub(O, s1), f3));
+        minv = d0; dir = f0; a1 = s0;
+        if (d1 < minv) { minv = d1; dir = f1; a1 = s0; }
+        if (d2 < minv) { minv = d2; dir = f2; a1 = s0; }
+        if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
+        if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
         T dt = dot(vsub(a1, O), dir);
         if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
-            T sx = 0, sy = 0, sz = 0;
-            if (iter == 1) {
-                // SUM over polytope(:,:,k), slot-major over faces: [s0 s0 s0 s1][s1 s2 s1 s2][s2 s3 s3 s3]
-                sx = ((((((((((s0.x + s0.x) + s0.x) + s1.x) + s1.x) + s2.x) + s1.x) + s2.x) + s2.x) + s3.x) + s3.x) + s3.x;
-                sy = ((((((((((s0.y + s0.y) + s0.y) + s1.y) + s1.y) + s2.y) + s1.y) + s2.y) + s2.y) + s3.y) + s3.y) + s3.y;
-                sz = ((((((((((s0.z + s0.z) + s0.z) + s1.z) + s1.z) + s2.z) + s1.z) + s2.z) + s2.z) + s3.z) + s3.z) + s3.z;
-            } else {
-                for (int j = 0; j < 3; ++j)
-                    for (int f = 0; f < F1; ++f) {
-                        V3<T> q = c.vert((int)((E.fv[f] >> (8 * j)) & 0xffu));
-                        sx += q.x; sy += q.y; sz += q.z;
-                    }
-            }
-            const T cnt = (T)(F1 * 3);
-            const V3<T> M = vmk<T>(sx / cnt, sy / cnt, sz / cnt);
-            dt = dot(vsub(a1, M), dir);
+            // SUM over polytope(:,:,k), slot-major over faces: [s0 s0 s0 s1][s1 s2 s1 s2][s2 s3 s3 s3]
+            const T sx = ((((((((((s0.x + s0.x) + s0.x) + s1.x) + s1.x) + s2.x) + s1.x) + s2.x) + s2.x) + s3.x) + s3.x) + s3.x;
+            const T sy = ((((((((((s0.y + s0.y) + s0.y) + s1.y) + s1.y) + s2.y) + s1.y) + s2.y) + s2.y) + s3.y) + s3.y) + s3.y;
+            const T sz = ((((((((((s0.z + s0.z) + s0.z) + s1.z) + s1.z) + s2.z) + s1.z) + s2.z) + s2.z) + s3.z) + s3.z) + s3.z;
+            const T cnt = (T)12;
+            dt = dot(vsub(a1, vmk<T>(sx / cnt, sy / cnt, sz / cnt)), dir);
         }
         if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
-        GK_STAMP(iter == 1 ? SE_IT1 : SE_DIR);
+        GK_STAMP(SE_IT1);
+        const V3<T> sp = support(c, dir);                          // :914
+        const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
+        // unique polytope vertices (getHullMeshesVertex, :920) + new point(s) -> ids 0..m-1
+        const bool u1 = !veq(s1, s0);
+        const bool u2 = !veq(s2, s0) && !veq(s2, s1);
+        const bool u3 = !veq(s3, s0) && !veq(s3, s1) && !veq(s3, s2);
+        const int i1 = 1, i2 = u1 ? 2 : 1, i3 = i2 + (u2 ? 1 : 0), isp = i3 + (u3 ? 1 : 0);
+        int m = isp + 1;
+        V3<T> sq = zero3<T>();
+        if (two) { sq = support(c, vneg(dir)); ++m; }
+        V3<T> q = s0;                                  // group lane j writes point j
+        bool w = gl == 0;
+        if (u1 && gl == i1) { q = s1; w = true; }
+        if (u2 && gl == i2) { q = s2; w = true; }
+        if (u3 && gl == i3) { q = s3; w = true; }
+        if (gl == isp) { q = sp; w = true; }
+        if (two && gl == isp + 1) { q = sq; w = true; }
+        if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
+        __builtin_amdgcn_wave_barrier();
+        GK_STAMP(SE_IT1);
+        const int st = hull_build(c, F, kbase, nv, nf, m);
+        if (st) return st;
+    }
+    int F1 = 4;
+    bool unchanged = false;
+    for (int iter = 1;; ++iter) {
+        // ---- end of iteration `iter`: MINLOC of the new polytope and the termination rules
+        const int F2 = nf;                                        // :956-969
+        face_argmin(c, F, minv, dir, a1);
+        V3<T> dir2 = dir;
+        if (c.g.unib(dot(vsub(a1, O), dir2) < T(0))) dir2 = vneg(dir2);
+        bool stop;                                                // :972-1015
+        if (F1 == F2) stop = unchanged || sorted_equal(c, F);    // unchanged hull: identical sorted lists
+        else stop = F1 > F2;
+        GK_STAMP(SE_TERM);
+        if (stop) { depth = minv; normal = dir2; return 0; }
+        // ---- iteration iter + 1: same faces as this iteration's F2, so its MINLOC carries over
+        iters = iter + 1;
+        if (iter + 1 > 99) return GJKEPA_STATUS_EPA_MAXITER;
+        F1 = nf;
+        T dt = dot(vsub(a1, O), dir);
+        if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(a1, polytope_centroid(c, F, F1)), dir);   // :905-908
+        if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+        GK_STAMP(SE_DIR);
         const V3<T> sp = support(c, dir);                          // :914
         GK_STAMP(SE_SUP);
         const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
-        int st;
-        if (iter == 1) {
-            // unique polytope vertices (getHullMeshesVertex, :920) + new point(s) -> ids 0..m-1
-            const bool u1 = !veq(s1, s0);
-            const bool u2 = !veq(s2, s0) && !veq(s2, s1);
-            const bool u3 = !veq(s3, s0) && !veq(s3, s1) && !veq(s3, s2);
-            const int i1 = 1, i2 = u1 ? 2 : 1, i3 = i2 + (u2 ? 1 : 0), isp = i3 + (u3 ? 1 : 0);
-            int m = isp + 1;
-            V3<T> sq = zero3<T>();
-            if (two) { sq = support(c, vneg(dir)); ++m; }
-            V3<T> q = s0;                                  // group lane j writes point j
-            bool w = gl == 0;
-            if (u1 && gl == i1) { q = s1; w = true; }
-            if (u2 && gl == i2) { q = s2; w = true; }
-            if (u3 && gl == i3) { q = s3; w = true; }
-            if (gl == isp) { q = sp; w = true; }
-            if (two && gl == isp + 1) { q = sq; w = true; }
-            if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
-            __builtin_amdgcn_wave_barrier();
-            GK_STAMP(SE_IT1);
-            st = hull_build(c, nv, nf, m);
-        } else {
-            if (two) {                    // net face count of two insertions unknown: save now
+        if (two) {                        // net face count of two insertions unknown: save now
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    int f = r * G + gl;
-                    if (f < nf) E.dsv[f] = E.fd[f];
-                }
+            for (int r = 0; r < R; ++r) {
+                const int f = r * G + gl;
+                if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
             }
-            bool ch1 = false, ch2 = false;
-            st = hull_add(c, nv, nf, sp, true, 0, ch1, !two);
-            if (!st && two) st = hull_add(c, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
-            unchanged = !ch1 && !ch2;
         }
+        bool ch1 = false, ch2 = false;
+        int st = hull_add(c, F, kbase, nv, nf, sp, true, 0, ch1, !two);
+        if (!st && two) st = hull_add(c, F, kbase, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
+        unchanged = !ch1 && !ch2;
         if (st) return st;
-        const int F2 = nf;                                        // :956-969
-        const int ml2 = face_argmin(c, nf);
-        const T minv2 = E.fd[ml2];
-        V3<T> dir2 = c.fn(ml2);
-        if (c.g.unib(dot(vsub(c.vert((int)(E.fv[ml2] & 0xffu)), O), dir2) < T(0))) dir2 = vneg(dir2);
-        ml_next = ml2;
-        bool stop;                                                // :972-1015
-        if (F1 == F2) stop = unchanged || sorted_equal(c, F1);   // unchanged hull: identical sorted lists
-        else stop = F1 > F2;
-        GK_STAMP(SE_TERM);
-        if (stop) { depth = minv2; normal = dir2; return 0; }
     }
 }
 
@@ -1067,15 +1195,18 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     const int gl = c.g.gl;
     gjk_it = 0;
     {   // RoughCollisionDetection_SphericalEnvelope (:1165-1188)
-        // the six sequential coordinate sums run on group lanes 0..5 (lane j: hull j/3, axis j%3)
-        T sum = 0;
-        if (gl < 6) {
-            const int h = gl / 3, ax = gl - 3 * (gl / 3);
-            const TH* col = ax == 0 ? L.hx[h] : ax == 1 ? L.hy[h] : L.hz[h];
-            const int n = h ? c.nb : c.na;
-            for (int i = 0; i < n; ++i) sum += (T)col[i];
-            sum = sum / (T)n;
-            L.u.g.l1[gl] = sum;
+        // the six sequential coordinate sums run on group lanes (sum j on lane j % G: hull j/3, axis j%3)
+#pragma unroll
+        for (int j0 = 0; j0 < 6; j0 += G) {
+            const int j = j0 + gl;
+            if (j < 6) {
+                const int h = j / 3, ax = j - 3 * (j / 3);
+                const TH* col = ax == 0 ? L.hx[h] : ax == 1 ? L.hy[h] : L.hz[h];
+                const int n = h ? c.nb : c.na;
+                T sum = 0;
+                for (int i = 0; i < n; ++i) sum += (T)col[i];
+                L.u.g.l1[j] = sum / (T)n;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         const V3<T> m1 = vmk<T>(L.u.g.l1[0], L.u.g.l1[1], L.u.g.l1[2]), m2 = vmk<T>(L.u.g.l1[3], L.u.g.l1[4], L.u.g.l1[5]);
@@ -1130,15 +1261,23 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     }
     GK_STAMP(SG_INIT);
     if (!enter) {
-        // cycle history (:193-194): group lane j < 12 keeps coordinate j of last1 / last2
-        T h1 = 0, h2 = 0;
-        const uint64_t m12 = 0xFFFull;
+        // cycle history (:193-194): coordinate j < 12 of last1 / last2 lives on group lane j % G,
+        // slot j / G
+        constexpr int HS = (12 + G - 1) / G;
+        T h1[HS], h2[HS];
+#pragma unroll
+        for (int t = 0; t < HS; ++t) { h1[t] = 0; h2[t] = 0; }
+        const uint64_t lowg = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
         const int sh = c.g.lane & ~(G - 1);
         for (int it = 1;; ++it) {                                        // :182-236
             gjk_it = it;
             if (it > 50) return PH_MISS;
-            h2 = h1;
-            h1 = simplex_coord(gl < 12 ? gl : 0, s0, s1, s2, s3);
+#pragma unroll
+            for (int t = 0; t < HS; ++t) {
+                const int j = t * G + gl;
+                h2[t] = h1[t];
+                h1[t] = simplex_coord(j < 12 ? j : 0, s0, s1, s2, s3);
+            }
             GK_STAMP(SG_CHK);
             update_simplex_c(c, nq, s0, s1, s2, s3, k0, k1, k2, k3);
             nq = quad_normal(q, s0, s1, s2, s3, mdq);
@@ -1149,9 +1288,16 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
             const V3<T> n = vmk<T>(qbcast<2>(nq.x), qbcast<2>(nq.y), qbcast<2>(nq.z));
             if (c.g.unib(fabs(dot(vsub(s3, s0), n)) < Tol<T>::PT)) return PH_MISS;         // :203-206
             if (c.g.unib(quad_inside(q, s0, s1, s2, s3, nq))) break;                      // :210-216
-            const T cur = simplex_coord(gl < 12 ? gl : 0, s0, s1, s2, s3);               // :219-234
-            const uint32_t e1 = (uint32_t)((__ballot(fabs(cur - h1) < Tol<T>::PT) >> sh) & m12);
-            const uint32_t e2 = (uint32_t)((__ballot(fabs(cur - h2) < Tol<T>::PT) >> sh) & m12);
+            uint32_t e1 = 0, e2 = 0;                                                       // :219-234
+#pragma unroll
+            for (int t = 0; t < HS; ++t) {
+                const int j = t * G + gl;
+                const T cur = simplex_coord(j < 12 ? j : 0, s0, s1, s2, s3);
+                e1 |= (uint32_t)((__ballot(fabs(cur - h1[t]) < Tol<T>::PT) >> sh) & lowg) << (t * G);
+                e2 |= (uint32_t)((__ballot(fabs(cur - h2[t]) < Tol<T>::PT) >> sh) & lowg) << (t * G);
+            }
+            e1 &= 0xFFFu;
+            e2 &= 0xFFFu;
             bool over = true;
 #pragma unroll
             for (int p = 0; p < 4; ++p) over = over && (((e1 >> (3 * p)) & 7u) == 7u || ((e2 >> (3 * p)) & 7u) == 7u);
@@ -1163,23 +1309,22 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
     return PH_HIT;
 }
 
-// EPA_solu (:242-346) from the GJK simplex.  Returns -type (OK, o13 filled), an error status or
-// ST_DEFER; `diag_epa` gets (epa_iters << 8) | (faces << 16).
-CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, int version, T tol_ff, T* o13, uint32_t& diag_epa) {
+// EPA_solu's polytope loop (:274-323) from the GJK simplex: 0 (depth, n filled), an error
+// status or ST_DEFER; `diag_epa` gets (epa_iters << 8) | (faces << 16).
+CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t& diag_epa) {
     const V3<T> s0 = decode_pt(c, kc[0]), s1 = decode_pt(c, kc[1]), s2 = decode_pt(c, kc[2]), s3 = decode_pt(c, kc[3]);
-    T depth = 0;
-    V3<T> n = zero3<T>();
+    depth = 0;
+    n = zero3<T>();
     int eit = 0, nf = 0;
-#ifdef GJKEPA_DIAG_GJK_ONLY   // timing ablation only (tools/build_variant.sh); never in the product build
-    return -1;
-#endif
-    int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf);
+    const int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf);
     diag_epa = ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
-    if (st) return st;
-    __builtin_amdgcn_wave_barrier();
-#ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
-    return -1;
-#endif
+    return st;
+}
+
+// EPA_solu's post-processing (:326-343) for EPA depth and normal n: nearest points, contact point
+// (version_ 1/2/3) and contact type.  Returns -type (o13 filled) or an error status.
+CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
+    int st;
     int ia, ib;
     GK_STAMP(SE_TERM);
     support_idx(c, n, ia, ib);                                           // get_nearest_points (:326, :813-855)
@@ -1194,6 +1339,7 @@ CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, int version, T tol_ff, T* o1
     const int type = collision_type(c, n, tol_ff);                        // :343
     GK_STAMP(SE_TYPE);
     const V3<T> q1 = c.A(ia), q2 = c.B(ib);
+    __builtin_amdgcn_wave_barrier();
     o13[0] = depth;
     o13[1] = n.x; o13[2] = n.y; o13[3] = n.z;
     o13[4] = pt.x; o13[5] = pt.y; o13[6] = pt.z;
@@ -1225,57 +1371,124 @@ CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restric
 }
 
 // record: 13 T fields, then int8 collision, type, status, reserved, uint32 diag, zero pad.
-// Group lane j < 16 stores one 8-byte (f64) / 4-byte (f32) word straight from registers.
-template <typename T> DEV void store_record(void* out, int64_t pair, int gl, const T* o13, int hit, int type,
-                                            int status, uint32_t diag) {
-    if (gl >= 16) return;
-    T v = T(0);
-#pragma unroll
-    for (int j = 0; j < 13; ++j) v = (gl == j) ? o13[j] : v;
+// Its 16 8-byte (f64) / 4-byte (f32) words are stored straight from registers, word j by group
+// lane j % G.
+template <int G, typename T> DEV void store_record(void* out, int64_t pair, int gl, const T* o13, int hit, int type,
+                                                   int status, uint32_t diag) {
     const uint32_t flags = (uint32_t)(hit & 0xff) | ((uint32_t)(type & 0xff) << 8) | ((uint32_t)(status & 0xff) << 16);
-    if constexpr (sizeof(T) == 8) {
-        uint64_t word = __builtin_bit_cast(uint64_t, v);
-        if (gl == 13) word = (uint64_t)flags | ((uint64_t)diag << 32);
-        if (gl > 13) word = 0;
-        reinterpret_cast<uint64_t*>(out)[pair * 16 + gl] = word;
-    } else {
-        uint32_t word = __builtin_bit_cast(uint32_t, v);
-        if (gl == 13) word = flags;
-        if (gl == 14) word = diag;
-        if (gl == 15) word = 0;
-        reinterpret_cast<uint32_t*>(out)[pair * 16 + gl] = word;
+#pragma unroll
+    for (int j0 = 0; j0 < 16; j0 += G) {
+        const int j = j0 + gl;
+        if (j >= 16) break;
+        T v = T(0);
+#pragma unroll
+        for (int i = 0; i < 13; ++i) v = (j == i) ? o13[i] : v;
+        if constexpr (sizeof(T) == 8) {
+            uint64_t word = __builtin_bit_cast(uint64_t, v);
+            if (j == 13) word = (uint64_t)flags | ((uint64_t)diag << 32);
+            if (j > 13) word = 0;
+            reinterpret_cast<uint64_t*>(out)[pair * 16 + j] = word;
+        } else {
+            uint32_t word = __builtin_bit_cast(uint32_t, v);
+            if (j == 13) word = flags;
+            if (j == 14) word = diag;
+            if (j == 15) word = 0;
+            reinterpret_cast<uint32_t*>(out)[pair * 16 + j] = word;
+        }
     }
 }
 
-DEV int epa_tier_for(int nmax) { return nmax <= GJKEPA_E0_G * GJKEPA_E0_K ? 0 : nmax <= GJKEPA_E1_G * GJKEPA_E1_K ? 1 : 2; }
+// hull capacity (vertices) of EPA tier t
+DEV constexpr int epa_hull_cap(int t) {
+    return t == 0 ? GJKEPA_E0_G * GJKEPA_E0_K : t == 1 ? GJKEPA_E1_G * GJKEPA_E1_K : t == 2 ? GJKEPA_E2_G * GJKEPA_E2_K
+                                                                                        : GJKEPA_E3_G * GJKEPA_E3_K;
+}
+static_assert(GJKEPA_E3_G * GJKEPA_E3_K >= GJKEPA_MAX_HULL_VERTS, "the last EPA tier must hold every hull");
+// smallest EPA tier >= t0 whose hull capacity holds nmax vertices
+DEV int epa_tier_for(int nmax, int t0 = 0) {
+    for (int t = t0; t < GJKEPA_EPA_TIERS - 1; ++t)
+        if (nmax <= epa_hull_cap(t)) return t;
+    return GJKEPA_EPA_TIERS - 1;
+}
 
-// Work distribution without atomics: every pair has a route byte (which kernel owns it next).  A
-// wave scans 64 consecutive route bytes with one coalesced load, ballots the matches and hands
-// them to its 64/G groups in pair order, one per group per round.  `route_code` < 0: every pair.
-// F(pair) runs for each pair the calling group receives.
+// Work distribution: runs of `claim` 64-pair chunks are handed out dynamically (one atomic per
+// wave per run on this launch's counter, prefetched one run ahead), so the launch ends within
+// about one run of its slowest wave.  Busy launches claim single chunks; launches that serve few
+// pairs claim long runs so the scan is not bound by atomics on one address.  Inside a chunk, the wave ballots the pairs whose route byte matches this
+// launch (one coalesced byte load) and hands them to its 64/G groups in pair order, one per group
+// per round.  `route_code` < 0: every pair.  F(pair) runs for each pair the calling group receives.
 template <int G, typename F>
-DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code, F&& f) {
+DEV void groups_take(const Grp<G>& grp, int64_t p0, uint64_t m, F&& f) {
     constexpr int GPW = 64 / G;
     const int gid = grp.lane / G;
+    while (m) {
+        // group g takes the g-th lowest set bit of m
+        uint64_t mm = m;
+        for (int j = 0; j < gid && mm; ++j) mm &= mm - 1;
+        const bool active = mm != 0;
+        const int bit = active ? (int)__builtin_ctzll(mm) : 0;
+        for (int j = 0; j < GPW && m; ++j) m &= m - 1;   // consume this round's GPW matches
+        if (active) f(p0 + bit);
+    }
+}
+// 16-bit mask of this lane's 16 route bytes equal to code
+DEV uint32_t match16(uint4 v, uint32_t code) {
+    uint32_t m = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m |= (((w[i >> 2] >> (8 * (i & 3))) & 0xffu) == code ? 1u : 0u) << i;
+    return m;
+}
+template <int G, typename F>
+DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code,
+                              uint32_t* ctr, int claim, F&& f) {
+    // the first unit of workgroup b is unit b; later units come from the counter (offset by the
+    // grid), so a launch with fewer units than workgroups issues no atomics at all
     const int64_t nchunks = (n_pairs + 63) / 64;
-    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const int64_t p0 = ch * 64;
-        uint64_t m;
-        if (route_code < 0) {
-            const int64_t left = n_pairs - p0;
-            m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
-        } else {
-            const int64_t p = p0 + grp.lane;
-            m = __ballot(p < n_pairs && (int)route[p] == route_code);
+    const int64_t nunits = claim <= 1 || route_code < 0 ? nchunks : (nchunks + 15) / 16;
+    uint32_t next = 0;
+    if ((int64_t)blockIdx.x < nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
+    if (claim <= 1 || route_code < 0) {
+        int64_t ch = blockIdx.x;
+        while (ch < nchunks) {
+            if (grp.lane == 0 && ch != (int64_t)blockIdx.x) next = gridDim.x + atomicAdd(ctr, 1u);   // prefetch
+            const int64_t p0 = ch * 64;
+            uint64_t m;
+            if (route_code < 0) {
+                const int64_t left = n_pairs - p0;
+                m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+            } else {
+                const int64_t p = p0 + grp.lane;
+                m = __ballot(p < n_pairs && (int)route[p] == route_code);
+            }
+            groups_take(grp, p0, m, f);
+            ch = (int64_t)__builtin_amdgcn_readfirstlane(next);
         }
-        while (m) {
-            // group g takes the g-th lowest set bit of m
-            uint64_t mm = m;
-            for (int j = 0; j < gid && mm; ++j) mm &= mm - 1;
-            const bool active = mm != 0;
-            const int bit = active ? (int)__builtin_ctzll(mm) : 0;
-            for (int j = 0; j < GPW && m; ++j) m &= m - 1;   // consume this round's GPW matches
-            if (active) f(p0 + bit);
+        return;
+    }
+    // runs of 16 chunks: lane l loads route bytes [16 l, 16 l + 16) of the run in one 16-byte load
+    for (int64_t run = blockIdx.x; run * 16 < nchunks; run = (int64_t)__builtin_amdgcn_readfirstlane(next)) {
+        if (grp.lane == 0 && run != (int64_t)blockIdx.x) next = gridDim.x + atomicAdd(ctr, 1u);
+        const int64_t q0 = run * 1024 + 16 * grp.lane;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (q0 + 16 <= n_pairs) {
+            v = *reinterpret_cast<const uint4*>(route + q0);
+        } else {
+            uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            for (int i = 0; i < 16; ++i)
+                if (q0 + i < n_pairs) w[i >> 2] = (w[i >> 2] & ~(0xffu << (8 * (i & 3)))) | ((uint32_t)route[q0 + i] << (8 * (i & 3)));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        const uint32_t mine = match16(v, (uint32_t)route_code);
+        uint64_t lanes = __ballot(mine != 0);                 // lanes 4j..4j+3 hold chunk j of the run
+        while (lanes) {
+            const int j = (int)__builtin_ctzll(lanes) >> 2;
+            lanes &= ~(0xFull << (4 * j));
+            uint64_t m = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                m |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mine, 4 * j + i) << (16 * i);
+            groups_take(grp, run * 1024 + 64 * j, m, f);
         }
     }
 }
@@ -1285,6 +1498,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
 // holds their hulls.  Tier 0 takes every pair; hulls above its capacity are routed to tier 1.
 template <typename TIn, typename T, int G, int K, int MINW>
 __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) {
+    static_assert(G >= 4, "the tetrahedron faces run on quads");
     using L_t = Lds<T, TIn, G, K, 4, 4>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
@@ -1292,7 +1506,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
         GK_STAMP(SG_ROUTE);
         Ctx<T, TIn, G, K, 4, 4> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1302,7 +1516,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
         uint8_t next = 0;
         if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
-            store_record<T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+            store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
         } else if (na > K * G || nb > K * G) {
             next = GJKEPA_ROUTE_GJK1;                        // larger GJK tier
         } else {
@@ -1311,7 +1525,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
             const bool bad_in = load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
             GK_STAMP(SG_LOAD);
             if (bad_in) {
-                store_record<T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+                store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
             } else {
                 uint32_t kc[4];
                 int gjk_it = 0;
@@ -1319,15 +1533,17 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                 __builtin_amdgcn_wave_barrier();
                 GK_STAMP(SG_CHK);
                 if (r == PH_HIT) {
-                    if (gl < 5) {
-                        const uint32_t word = gl == 0 ? kc[0] : gl == 1 ? kc[1] : gl == 2 ? kc[2] : gl == 3 ? kc[3] : (uint32_t)gjk_it;
-                        reinterpret_cast<uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + gl] = word;
+#pragma unroll
+                    for (int j0 = 0; j0 < 5; j0 += G) {
+                        const int j = j0 + gl;
+                        const uint32_t word = j == 0 ? kc[0] : j == 1 ? kc[1] : j == 2 ? kc[2] : j == 3 ? kc[3] : (uint32_t)gjk_it;
+                        if (j < 5) reinterpret_cast<uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + j] = word;
                     }
                     next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(na > nb ? na : nb));
                 } else if (r == PH_MISS) {
-                    store_record<T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
+                    store_record<G, T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
                 } else {                                  // GJK-phase error (reference would STOP)
-                    store_record<T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
+                    store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
                 }
             }
         }
@@ -1339,8 +1555,11 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     GK_STAMP_END();
 }
 
-// EPA kernel: EPA + contact features for the pairs routed to this tier.  A polytope that outgrows
-// the tier is routed to the next one (recomputed from the same simplex codes).
+DEV int contact_tier_for(int nmax) { return nmax <= GJKEPA_C0_G * GJKEPA_C0_K ? 0 : 1; }
+
+// EPA kernel: the polytope loop for the pairs routed to this tier.  Depth, normal and the
+// diagnostics are parked in their final record fields and the pair goes to its contact tier.  A
+// polytope that outgrows the tier is routed to the next one (recomputed from the simplex codes).
 template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW>
 __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, VC, FC>;
@@ -1350,39 +1569,92 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, [&](int64_t pair) {
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, VC, FC> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
         c.nb = grp.uni(a.hull_cnt[hb]);
-        const uint32_t* slot = reinterpret_cast<const uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
+        uint32_t* slot = reinterpret_cast<uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
         uint32_t kc[4];
         kc[0] = slot[0]; kc[1] = slot[1]; kc[2] = slot[2]; kc[3] = slot[3];
         const uint32_t gjk_it = slot[4];
         load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
-        T o13[13];
-#pragma unroll
-        for (int i = 0; i < 13; ++i) o13[i] = T(0);
+        T depth;
+        V3<T> n;
         uint32_t de = 0;
         GK_STAMP(SE_LOAD);
-        const int r = epa_phase(c, kc, a.version, (T)a.tol_ff, o13, de);
+#ifdef GJKEPA_DIAG_GJK_ONLY   // timing ablation only (tools/build_variant.sh); never in the product build
+        const int r = GJKEPA_STATUS_DEGENERATE;
+        depth = 0; n = zero3<T>();
+#else
+        const int r = (c.na > G * K || c.nb > G * K) ? ST_DEFER : epa_phase(c, kc, depth, n, de);
+#endif
         __builtin_amdgcn_wave_barrier();
+        const uint32_t diag = (gjk_it & 0xffu) | de;
         uint8_t next = 0;
-        if (r == ST_DEFER && a.next_code >= 0) {
-            next = (uint8_t)a.next_code;
-        } else if (r == ST_DEFER) {                       // last tier: capacity exhausted
+        if (r == ST_DEFER && a.next_code >= 0) {   // next tier that holds the hulls
+            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0));
+        } else if (r == 0) {
+            // park depth, normal (record fields 0..3) and diag; the contact tier finishes the record
+            T* rec = reinterpret_cast<T*>(slot);
+            if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
+            if (gl == 4) slot[sizeof(T) == 8 ? 27 : 14] = diag;
+            next = (uint8_t)(GJKEPA_ROUTE_CT0 + contact_tier_for(c.na > c.nb ? c.na : c.nb));
+        } else {                 // error status (last tier out of capacity: DEGENERATE): outputs zero, collision = 1
+            T o13[13];
 #pragma unroll
             for (int i = 0; i < 13; ++i) o13[i] = T(0);
-            store_record<T>(a.out, pair, gl, o13, 1, 0, GJKEPA_STATUS_DEGENERATE, (gjk_it & 0xffu) | de);
-        } else if (r < 0) {
-            store_record<T>(a.out, pair, gl, o13, 1, -r, 0, (gjk_it & 0xffu) | de);
-        } else {                                          // error status: outputs zero, collision = 1
-#pragma unroll
-            for (int i = 0; i < 13; ++i) o13[i] = T(0);
-            store_record<T>(a.out, pair, gl, o13, 1, 0, r, (gjk_it & 0xffu) | de);
+            store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
         }
         if (gl == 0) a.route[pair] = next;
+        __builtin_amdgcn_wave_barrier();
+        GK_STAMP(SE_STORE);
+    });
+    GK_STAMP(SE_ROUTE);
+    GK_STAMP_END();
+}
+
+// Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
+// finished, from the depth and normal it parked; writes the final record.
+template <typename TIn, typename T, int G, int K, int MINW>
+__global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args a) {
+    using L_t = Lds<T, TIn, G, K, 4, 4>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<G> grp;
+    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    const int gl = grp.gl;
+    const TIn* verts = (const TIn*)a.verts;
+    GK_STAMP_BEGIN();
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
+        GK_STAMP(SE_ROUTE);
+        Ctx<T, TIn, G, K, 4, 4> c{L, grp};
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        c.na = grp.uni(a.hull_cnt[ha]);
+        c.nb = grp.uni(a.hull_cnt[hb]);
+        const T* rec = reinterpret_cast<const T*>(a.out) + pair * 16;     // 16 T fields per record
+        const T depth = rec[0];
+        const V3<T> n = vmk<T>(rec[1], rec[2], rec[3]);
+        const uint32_t diag = reinterpret_cast<const uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + (sizeof(T) == 8 ? 27 : 14)];
+        load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+        GK_STAMP(SE_LOAD);
+        T o13[13];
+#ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
+        const int r = -1;
+#pragma unroll
+        for (int i = 0; i < 13; ++i) o13[i] = T(0);
+#else
+        const int r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
+#endif
+        __builtin_amdgcn_wave_barrier();
+        if (r < 0) {
+            store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
+        } else {                 // error status: outputs zero, collision = 1
+#pragma unroll
+            for (int i = 0; i < 13; ++i) o13[i] = T(0);
+            store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, diag);
+        }
+        if (gl == 0) a.route[pair] = 0;
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SE_STORE);
     });
@@ -1433,6 +1705,23 @@ hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
     return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW>(a, s)
                      : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW>(a, s);
 }
+template <typename TIn, typename T, int G, int K, int MINW>
+hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
+    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW>;
+    constexpr int GPW = 64 / G;
+    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 4, 4>) * GPW;
+    int grid = grid_for(kfn, lds, a.num_cus, a.grid);
+    const int64_t chunks = (a.n_pairs + 63) / 64;
+    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
+    return hipGetLastError();
+}
+template <typename TIn, typename T>
+hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
+    return tier == 0 ? launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW>(a, s)
+                     : launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW>(a, s);
+}
+
 template <typename TIn, typename T>
 hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
@@ -1467,4 +1756,10 @@ hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjke
     if (vert_dtype == GJKEPA_DTYPE_F32)
         return precision == GJKEPA_PREC_F64 ? epa_any<float, double>(tier, a, s) : epa_any<float, float>(tier, a, s);
     return precision == GJKEPA_PREC_F64 ? epa_any<double, double>(tier, a, s) : epa_any<double, float>(tier, a, s);
+}
+
+hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
+    if (vert_dtype == GJKEPA_DTYPE_F32)
+        return precision == GJKEPA_PREC_F64 ? contact_any<float, double>(tier, a, s) : contact_any<float, float>(tier, a, s);
+    return precision == GJKEPA_PREC_F64 ? contact_any<double, double>(tier, a, s) : contact_any<double, float>(tier, a, s);
 }
