@@ -418,8 +418,8 @@ template <typename T> DEV T qnan() { return __builtin_nan(""); }
 // HULL) are removed and the horizon is coned to k.  `changed` reports whether the hull changed;
 // with `save_eq` the current distances are saved to dsv[] when the face count will not change
 // (the only case the termination test reads them).
-CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3<T> p, bool append, int kexist,
-                       bool& changed, bool save_eq) {
+CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, int& nf, V3<T> p, bool append,
+                       int kexist, bool& changed, bool save_eq) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
@@ -449,12 +449,17 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3
         if (gl == 0) { E.vx[k] = p.x; E.vy[k] = p.y; E.vz[k] = p.z; }
         nv = nv + 1;
     }
+    int vp[R];               // position of this slot's face in the visible list, -1 if not visible
     {   // visible faces (ids, key) in slot order
         int base = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            vp[r] = -1;
             if (!live[r]) continue;
-            if (c.g.bit(vm[r])) E.x.h.visl[base + mbcnt(vm[r])] = (uint64_t)F.fv[r] | ((uint64_t)F.key[r] << 32);
+            if (c.g.bit(vm[r])) {
+                vp[r] = base + mbcnt(vm[r]);
+                E.x.h.visl[vp[r]] = (uint64_t)F.fv[r] | ((uint64_t)F.key[r] << 32);
+            }
             base += popc(vm[r]);
         }
     }
@@ -510,26 +515,39 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3
     __builtin_amdgcn_wave_barrier();
     GK_STAMP(SE_CMP);
     // New faces (horizon edge h coned to k) are built G at a time on group lane h % G and staged
-    // in LDS; the visible faces go and the new faces take the first nh free slots in slot order.
+    // in LDS, then copied into their slots.  Placement (results do not depend on it: the keys
+    // carry the order): new face h takes the slot of visible face h, the ones beyond nvis are
+    // appended at the high-water mark hw; a visible slot left over becomes a hole.  When the
+    // append would pass FC, the new faces take the first nh free slots (holes included).
     const V3<T> P = c.vert(k);
     bool bad = false;
-    int fr[R];
-    {
-        int fbase = 0;
+    int tj[R];               // index of the new face this slot receives, -1 if none
+    const int app = nh - nvis;
+    if (hw + (app > 0 ? app : 0) <= FC) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (!live[r] && (r + 1) * G <= FC) {   // every slot of the row is free
-                fr[r] = fbase + gl;
-                fbase += G;
-                continue;
-            }
-            const bool vis = c.g.bit(vm[r]);
+            const int slot = r * G + gl;
+            int h = vp[r];
+            if (h < 0 && slot >= hw && slot < hw + app) h = nvis + slot - hw;
+            tj[r] = h < nh ? h : -1;
+            if (vp[r] >= 0) F.fv[r] = kEmpty;
+        }
+        if (app > 0) hw += app;
+    } else {
+        int fbase = 0, top = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool vis = vp[r] >= 0;
             const bool fre = ((F.fv[r] & kEmpty) || vis) && (r * G + gl < FC);
             const uint64_t fm = c.g.ballot(fre);
-            fr[r] = fre ? fbase + mbcnt(fm) : 0x7fffffff;
+            const int fr = fbase + mbcnt(fm);
             fbase += popc(fm);
+            tj[r] = fre && fr < nh ? fr : -1;
+            if (tj[r] >= 0) top = r * G + gl + 1;
             if (vis) F.fv[r] = kEmpty;
         }
+        top = gmax<G>(top);
+        hw = hw > top ? hw : top;
     }
     for (int h0 = 0; h0 < nh; h0 += G) {
         const int h = h0 + gl;
@@ -547,8 +565,8 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int j = fr[r] - h0;
-            const bool tgt = j >= 0 && j < G && fr[r] < nh;
+            const int j = tj[r] - h0;
+            const bool tgt = j >= 0 && j < G;
             if (__ballot(tgt)) {
                 if (tgt) {
                     F.nx[r] = E.x.h.sn[j][0]; F.ny[r] = E.x.h.sn[j][1]; F.nz[r] = E.x.h.sn[j][2];
@@ -569,7 +587,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, V3
 // Hull of <= 6 points from scratch (EPA iteration 1): the points are vertex ids 0..m-1 of the
 // polytope.  First non-degenerate tetrahedron in list order, faces in the seed pattern of
 // :279-293 wound outward (slots / keys 0..3), then the remaining points in order.
-CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, int m) {
+CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, int& nf, int m) {
     constexpr int R = (FC + G - 1) / G;
     nv = m;
     nf = 0;
@@ -612,10 +630,11 @@ CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& nv, int& nf, 
     if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
     nf = 4;
     kbase = 4;
+    hw = 4;
     for (int j = 1; j < m; ++j) {
         if (j == i1 || j == i2 || j == i3) continue;
         bool ch;
-        int st = hull_add(c, F, kbase, nv, nf, c.vert(j), false, j, ch, false);
+        int st = hull_add(c, F, kbase, hw, nv, nf, c.vert(j), false, j, ch, false);
         if (st) return st;
     }
     return 0;
@@ -747,7 +766,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
         const int f = r * G + gl;
         if (f < FC) E.dsv[f] = qnan<T>();
     }
-    int nv = 0;
+    int nv = 0, hw = 0;
     uint32_t kbase = 0;
     nf = 0;
     T minv = 0;
@@ -796,7 +815,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
         if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SE_IT1);
-        const int st = hull_build(c, F, kbase, nv, nf, m);
+        const int st = hull_build(c, F, kbase, hw, nv, nf, m);
         if (st) return st;
     }
     int F1 = 4;
@@ -831,8 +850,8 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
             }
         }
         bool ch1 = false, ch2 = false;
-        int st = hull_add(c, F, kbase, nv, nf, sp, true, 0, ch1, !two);
-        if (!st && two) st = hull_add(c, F, kbase, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
+        int st = hull_add(c, F, kbase, hw, nv, nf, sp, true, 0, ch1, !two);
+        if (!st && two) st = hull_add(c, F, kbase, hw, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
         unchanged = !ch1 && !ch2;
         if (st) return st;
     }
