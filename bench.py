@@ -159,20 +159,26 @@ def main():
 
     bpq = algorithmic_bytes_per_query(float(pool.hull_cnt.sum()) / n, 4, rec_bytes)
     achieved = n * bpq / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM traffic and VALU issue of the same chain from the committed PMC run (tools/pmc.sh +
+    # tools/pmc_report.py, keyed by precision/config/batch size); null when none matches
+    traffic, valu = None, None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
-            pj = json.load(open(prof))
-            key = f"{args.precision}_{args.config}_{n}"
-            if key in pj:
-                traffic = pj[key]["bytes_per_launch"]
+            pj = json.load(open(prof)).get(f"{args.precision}_{args.config}_{n}")
+            if pj:
+                traffic = pj["bytes_per_launch"]
+                if pj.get("valu_instr"):
+                    valu = {"instr_per_query": round(pj["valu_instr_per_query"], 1),
+                            "issue_frac_pmc": round(pj["valu_issue_frac"], 4),
+                            "issue_frac_live": round(pj["valu_instr"] * 2.0 / (1024 * kern_ms * 1e-3 * 2.4e9), 4),
+                            "note": "SQ_INSTS_VALU priced at the 2-cycle wave64 issue slot vs 1024 SIMDs x kernel time x 2.4 GHz"}
         except Exception:
-            traffic = None
+            traffic, valu = None, None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic,
+                "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic, "valu_issue": valu,
                 "bytes_per_query": round(bpq, 1), "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
-                "kernel": "gjk_kernel + epa_kernel tiers (one launch chain; HIP events on the launch stream)"}
+                "kernel": "gjk + epa + contact kernel tiers (one launch chain; HIP events on the launch stream)"}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "M queries/s", "n_gpus": world,

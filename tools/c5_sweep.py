@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Config C5: deep-overlap pairs, fp64 vs fp32 compute against the oracle.
+
+Runs the C5 workload (hull B offset r ~ U[0, 0.3], 32-128-vertex hulls, every pair a hit) through
+the GPU path in fp64 and fp32 compute, compares both with the fp64 oracle on the same pairs and
+reports: hit / type agreement, the fraction of byte-identical records, and error CDFs of the
+penetration depth (relative) and of the normal (angle), for all pairs and for the subset whose
+final polytope has >= 64 faces.  Also times both precisions on the GPU.  Writes one JSON file.
+usage: python tools/c5_sweep.py [n_pairs] [out.json]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "collision-detect-gjk-epa_amd"), os.path.join(ROOT, "oracle")]
+import gjkepa  # noqa: E402
+import oracle  # noqa: E402  (checker only)
+
+SEED = 0x6A4B5C1D
+QS = (0.5, 0.9, 0.99, 0.999, 1.0)
+
+
+def cdf(x):
+    x = np.asarray(x, float)
+    if x.size == 0:
+        return {}
+    return {f"p{int(q * 1000) / 10:g}" if q < 1 else "max": float(np.quantile(x, q)) for q in QS}
+
+
+def errors(g, r, mask):
+    g, r = g[mask], r[mask]
+    both = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
+    gd, rd = g["penetration_depth"][both].astype(np.float64), r["penetration_depth"][both]
+    rel = np.abs(gd - rd) / np.maximum(np.abs(rd), 1e-300)
+    gn = g["collision_normal"][both].astype(np.float64)
+    rn = r["collision_normal"][both]
+    cosang = np.clip(np.sum(gn * rn, axis=1) / np.maximum(np.linalg.norm(gn, axis=1) * np.linalg.norm(rn, axis=1), 1e-300), -1, 1)
+    ang = np.arccos(cosang)
+    return {
+        "pairs": int(mask.sum()),
+        "hit_agreement": float((g["collision"] == r["collision"]).mean()) if mask.any() else None,
+        "type_agreement": float((g["colli_type"] == r["colli_type"]).mean()) if mask.any() else None,
+        "status_agreement": float((g["status"] == r["status"]).mean()) if mask.any() else None,
+        "depth_rel_err": cdf(rel),
+        "normal_angle_err_rad": cdf(ang),
+    }
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "c5_fp32_sweep.json")
+    pool = gjkepa.synth_pairs(SEED, n, 32, 128, 0.3, dtype=np.float32)
+    res = {"workload": f"C5: {n} pairs, hulls 32-128 vertices, hull B offset r~U[0,0.3], fp32 vertex storage, "
+                       f"version_=2, TOL_FF_=1.0, seed {SEED:#x}", "reference": "fp64 oracle restatement (oracle/)"}
+    t = time.perf_counter()
+    ref = oracle.gjkepa_batch(pool, 2, 1.0, min(os.cpu_count() or 1, 16))
+    res["oracle_seconds"] = time.perf_counter() - t
+    faces = (ref["diag"] >> 16).astype(np.int64)
+    deep = faces >= 64
+    res["final_faces"] = {"mean": float(faces.mean()), "frac_ge_64": float(deep.mean()), **cdf(faces)}
+    for name, prec in (("fp64", gjkepa.PREC_F64), ("fp32", gjkepa.PREC_F32)):
+        gjkepa.gjkepa_batch(pool, 2, 1.0, precision=prec)            # warm
+        t = time.perf_counter()
+        g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=prec)
+        dt = time.perf_counter() - t
+        entry = {"host_api_Mq_per_s_incl_transfers": n / dt / 1e6,
+                 "all": errors(g, ref, np.ones(n, bool)), "faces_ge_64": errors(g, ref, deep)}
+        if prec == gjkepa.PREC_F64:
+            entry["bitexact_records"] = float((np.frombuffer(g.tobytes(), np.uint8).reshape(n, -1) ==
+                                               np.frombuffer(ref.tobytes(), np.uint8).reshape(n, -1)).all(axis=1).mean())
+        res[name] = entry
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

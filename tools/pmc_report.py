@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Per-launch-chain PMC summary of a tools/pmc.sh run, for bench.py's roofline fields.
+
+Every kernel of the GJK/EPA/contact chain is dispatched once per bench step; counters are
+averaged over a kernel's dispatches and summed over the chain.  HBM traffic follows
+/opt/skills/guides/MI355X_MICROARCH.md (§HBM): FETCH_SIZE and WRITE_SIZE are KiB, and on gfx950
+FETCH_SIZE counts half the bytes of wide reads, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+VALU issue: SQ_INSTS_VALU wave-instructions; `valu_issue_frac` prices each at the 2-cycle wave64
+issue slot (32 lanes/clock) against 1024 SIMDs x the chain's kernel time x 2.4 GHz (fp64 ops take
+longer, so this is a lower bound on VALU-pipe occupancy).
+usage: python tools/pmc_report.py <gpurun_out tag> <key> <n_pairs>  (merges into profiles/pmc_traffic.json)"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag, key, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    base = os.path.join(ROOT, "gpurun_out", tag, "pmc")
+    per = collections.defaultdict(lambda: collections.defaultdict(dict))
+    dur = collections.defaultdict(dict)
+    for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "gk::" not in r["Kernel_Name"]:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            d = per[k][r["Counter_Name"]]
+            d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    for f in sorted(glob.glob(f"{base}/p*/run_kernel_trace.csv")):
+        for r in csv.DictReader(open(f)):
+            if "gk::" not in r["Kernel_Name"]:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            dur[k][f + r.get("Dispatch_Id", "")] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    kernels = {}
+    for k, cs in per.items():
+        kernels[k] = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+        if dur.get(k):
+            kernels[k]["seconds"] = sum(dur[k].values()) / len(dur[k])
+    tot = collections.Counter()
+    for m in kernels.values():
+        tot.update(m)
+    traffic = (2.0 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0
+    secs = tot["seconds"]
+    entry = {
+        "bytes_per_launch": traffic,
+        "fetch_bytes_corrected": 2.0 * tot["FETCH_SIZE"] * 1024.0,
+        "write_bytes": tot["WRITE_SIZE"] * 1024.0,
+        "valu_instr": tot["SQ_INSTS_VALU"],
+        "valu_instr_per_query": tot["SQ_INSTS_VALU"] / n,
+        "chain_kernel_seconds": secs,
+        "valu_issue_frac": tot["SQ_INSTS_VALU"] * 2.0 / (1024 * secs * 2.4e9) if secs else None,
+        "kernels": kernels,
+        "source": f"tools/pmc.sh run {tag}, kernels averaged per dispatch, summed over the chain",
+    }
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    allj = json.load(open(path)) if os.path.exists(path) else {}
+    allj[key] = entry
+    json.dump(allj, open(path, "w"), indent=1)
+    print(json.dumps({k: v for k, v in entry.items() if k != "kernels"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
