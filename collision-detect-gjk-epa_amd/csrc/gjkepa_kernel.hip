@@ -239,8 +239,13 @@ template <int S, int N, typename T> DEV void min_steps(T& v) {
 template <int G, typename T> DEV T gmin(T v) { min_steps<0, Grp<G>::kSteps>(v); return v; }
 
 // ---------------------------------------------------------------- per-group LDS image
-template <typename T, typename TH, int G, int K, int VC, int FC> struct Lds {
+// Sized for the kernel that uses it: VC > 0 is the EPA polytope (VC vertices, FC face slots);
+// VC == 0 is the GJK kernel (FC == 0) or the contact kernel (FC == 1), which carry only their own
+// scratch, so a 16-pair GJK wave does not pay for polytope or contact arrays.
+template <typename T, typename TH, int G, int K, int VC_, int FC_> struct Lds {
     static constexpr int NH = G * K;
+    static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 ? G : 1;
+    static constexpr int NC = (VC_ == 0 && FC_ == 1) ? NH : 1;
     TH hx[2][NH], hy[2][NH], hz[2][NH];  // hull A (0) / B (1) vertices, storage precision
     union U {
         struct E {                       // EPA polytope (faces themselves are in registers)
@@ -252,15 +257,15 @@ template <typename T, typename TH, int G, int K, int VC, int FC> struct Lds {
                 struct H {                                                                 // hull_add lists
                     uint64_t visl[FC];                       // visible faces: ids | key << 32
                     uint32_t horu[FC], hork[FC];             // horizon edges: u | w << 8, new face key
-                    T sn[G][4];                              // new faces of one round: normal, |distance|
-                    uint32_t sv[G], sk[G];                   //   ids, key
+                    T sn[GS][4];                             // new faces of one round: normal, |distance|
+                    uint32_t sv[GS], sk[GS];                 //   ids, key
                 } h;
                 struct S { T cur[FC]; T srt[FC]; } s;                                     // sorted_equal
                 struct O { uint32_t key[FC]; uint32_t ord[FC]; } o;                       // centroid order
             } x;
         } e;
         struct Gh { T l1[12], l2[12]; } g;   // GJK simplex history (:193-194)
-        struct C { T sx[NH], sy[NH], sz[NH], pol[NH]; uint32_t ord[NH]; } c;   // contact features
+        struct C { T sx[NC], sy[NC], sz[NC], pol[NC]; uint32_t ord[NC]; } c;   // contact features
     } u;
 };
 
@@ -1518,7 +1523,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
 template <typename TIn, typename T, int G, int K, int MINW>
 __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) {
     static_assert(G >= 4, "the tetrahedron faces run on quads");
-    using L_t = Lds<T, TIn, G, K, 4, 4>;
+    using L_t = Lds<T, TIn, G, K, 0, 0>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
     L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
@@ -1527,7 +1532,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     GK_STAMP_BEGIN();
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
         GK_STAMP(SG_ROUTE);
-        Ctx<T, TIn, G, K, 4, 4> c{L, grp};
+        Ctx<T, TIn, G, K, 0, 0> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
         T o13[13];
@@ -1638,7 +1643,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
 // finished, from the depth and normal it parked; writes the final record.
 template <typename TIn, typename T, int G, int K, int MINW>
 __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args a) {
-    using L_t = Lds<T, TIn, G, K, 4, 4>;
+    using L_t = Lds<T, TIn, G, K, 0, 1>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
     L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
@@ -1647,7 +1652,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     GK_STAMP_BEGIN();
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
-        Ctx<T, TIn, G, K, 4, 4> c{L, grp};
+        Ctx<T, TIn, G, K, 0, 1> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
         c.nb = grp.uni(a.hull_cnt[hb]);
@@ -1697,7 +1702,7 @@ template <typename TIn, typename T, int G, int K, int MINW>
 hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     auto kfn = gk::gjk_kernel<TIn, T, G, K, MINW>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 4, 4>) * GPW;
+    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 0, 0>) * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
     const int64_t chunks = (a.n_pairs + 63) / 64;
     if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
@@ -1728,7 +1733,7 @@ template <typename TIn, typename T, int G, int K, int MINW>
 hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     auto kfn = gk::contact_kernel<TIn, T, G, K, MINW>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 4, 4>) * GPW;
+    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 0, 1>) * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
     const int64_t chunks = (a.n_pairs + 63) / 64;
     if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
