@@ -216,6 +216,16 @@ def main():
         result["fp32_compute"] = {"value": round(n / (ms32 * 1e-3) / 1e6, 3), "unit": "M queries/s",
                                   "hit_agreement_vs_f64": round(float((r32["collision"] == recs["collision"]).mean()), 6)}
 
+    # host-buffer entry point (gjkepa_batch: H2D copy of hulls/pairs, kernels, D2H of records):
+    # the PCIe-inclusive rate, reported beside `value`, never as it
+    if rank == 0 and world == 1 and not args.no_f32_leg:
+        gjkepa.gjkepa_batch(pool, args.version, 1.0, precision=prec)
+        t = time.perf_counter()
+        for _ in range(2):
+            gjkepa.gjkepa_batch(pool, args.version, 1.0, precision=prec)
+        result["host_api"] = {"value": round(2 * n / (time.perf_counter() - t) / 1e6, 3), "unit": "M queries/s",
+                              "note": "gjkepa_batch on host buffers, PCIe transfers included"}
+
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # checker / CPU baseline only
