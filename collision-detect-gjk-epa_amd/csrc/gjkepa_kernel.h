@@ -44,6 +44,9 @@
 #ifndef GJKEPA_E0_MINW
 #define GJKEPA_E0_MINW 2
 #endif
+#ifndef GJKEPA_E0_REFILL
+#define GJKEPA_E0_REFILL 2      // refill a wave's groups once this many are idle (0: per-round kernel)
+#endif
 #ifndef GJKEPA_E1_G
 #define GJKEPA_E1_G 32
 #endif
@@ -91,10 +94,10 @@
 #endif
 // contact-feature tiers (nearest points, contact point, contact type): G, K as above
 #ifndef GJKEPA_C0_G
-#define GJKEPA_C0_G 16
+#define GJKEPA_C0_G 8
 #endif
 #ifndef GJKEPA_C0_K
-#define GJKEPA_C0_K 2
+#define GJKEPA_C0_K 4
 #endif
 #ifndef GJKEPA_C0_MINW
 #define GJKEPA_C0_MINW 2

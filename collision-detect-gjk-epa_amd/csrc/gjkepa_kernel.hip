@@ -757,109 +757,133 @@ CTX_T DEV V3<T> polytope_centroid(CTX& c, const FACES_T& F, int nf) {
     return vmk<T>(sx / cnt, sy / cnt, sz / cnt);
 }
 
-// EPA_solu loop (:274-323) + update_expandingPolytope_EPA (:863-1022).  Iteration 1 (seed soup
-// and hull from scratch) is peeled so the GJK simplex is dead inside the loop.
-CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf) {
+// EPA_solu loop (:274-323) + update_expandingPolytope_EPA (:863-1022) as a resumable state
+// machine: epa_begin runs iteration 1 (seed soup and hull from scratch), epa_step closes the
+// current iteration (MINLOC of the new polytope, termination rules) and, unless it stopped, runs
+// the next one.  A group can therefore be refilled with a new pair between any two iterations.
+constexpr int ST_CONT = 101;     // internal: EPA continues
+
+template <typename T, int R> struct EpaState {
+    Faces<T, R> F;
+    int nv, hw, nf, F1, iters;
+    uint32_t kbase;
+    T minv;
+    V3<T> dir, a1;                 // MINLOC face of the current polytope (normal, first vertex)
+    bool unchanged;
+};
+#define EPAST_T EpaState<T, (FC + G - 1) / G>
+
+CTX_T DEV int epa_begin(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const V3<T> O = zero3<T>();
     const int gl = c.g.gl;
-    FACES_T F;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        F.fv[r] = kEmpty;
+        S.F.fv[r] = kEmpty;
         const int f = r * G + gl;
         if (f < FC) E.dsv[f] = qnan<T>();
     }
-    int nv = 0, hw = 0;
-    uint32_t kbase = 0;
-    nf = 0;
-    T minv = 0;
-    V3<T> dir = O, a1 = O;           // MINLOC face of the current polytope (normal, first vertex)
-    iters = 1;
-    {   // ---- iteration 1
-        // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN
-        const V3<T> f0 = uninml(s0, s1, s2), f1 = uninml(s0, s2, s3), f2 = uninml(s0, s1, s3), f3 = uninml(s1, s2, s3);
-        if (c.g.unib(is_zero_nml(f0) || is_zero_nml(f1) || is_zero_nml(f2) || is_zero_nml(f3)))
-            return GJKEPA_STATUS_DEGENERATE;
-        const T d0 = fabs(dot(vsub(O, s0), f0)), d1 = fabs(dot(vsub(O, s0), f1));
-        const T d2 = fabs(dot(vsub(O, s0), f2)), d3 = fabs(dot(vsub(O, s1), f3));
-        minv = d0; dir = f0; a1 = s0;
-        if (d1 < minv) { minv = d1; dir = f1; a1 = s0; }
-        if (d2 < minv) { minv = d2; dir = f2; a1 = s0; }
-        if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
-        if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
-        T dt = dot(vsub(a1, O), dir);
-        if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
-            // SUM over polytope(:,:,k), slot-major over faces: [s0 s0 s0 s1][s1 s2 s1 s2][s2 s3 s3 s3]
-            const T sx = ((((((((((s0.x + s0.x) + s0.x) + s1.x) + s1.x) + s2.x) + s1.x) + s2.x) + s2.x) + s3.x) + s3.x) + s3.x;
-            const T sy = ((((((((((s0.y + s0.y) + s0.y) + s1.y) + s1.y) + s2.y) + s1.y) + s2.y) + s2.y) + s3.y) + s3.y) + s3.y;
-            const T sz = ((((((((((s0.z + s0.z) + s0.z) + s1.z) + s1.z) + s2.z) + s1.z) + s2.z) + s2.z) + s3.z) + s3.z) + s3.z;
-            const T cnt = (T)12;
-            dt = dot(vsub(a1, vmk<T>(sx / cnt, sy / cnt, sz / cnt)), dir);
-        }
-        if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
-        GK_STAMP(SE_IT1);
-        const V3<T> sp = support(c, dir);                          // :914
-        const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
-        // unique polytope vertices (getHullMeshesVertex, :920) + new point(s) -> ids 0..m-1
-        const bool u1 = !veq(s1, s0);
-        const bool u2 = !veq(s2, s0) && !veq(s2, s1);
-        const bool u3 = !veq(s3, s0) && !veq(s3, s1) && !veq(s3, s2);
-        const int i1 = 1, i2 = u1 ? 2 : 1, i3 = i2 + (u2 ? 1 : 0), isp = i3 + (u3 ? 1 : 0);
-        int m = isp + 1;
-        V3<T> sq = zero3<T>();
-        if (two) { sq = support(c, vneg(dir)); ++m; }
-        V3<T> q = s0;                                  // group lane j writes point j
-        bool w = gl == 0;
-        if (u1 && gl == i1) { q = s1; w = true; }
-        if (u2 && gl == i2) { q = s2; w = true; }
-        if (u3 && gl == i3) { q = s3; w = true; }
-        if (gl == isp) { q = sp; w = true; }
-        if (two && gl == isp + 1) { q = sq; w = true; }
-        if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
-        __builtin_amdgcn_wave_barrier();
-        GK_STAMP(SE_IT1);
-        const int st = hull_build(c, F, kbase, hw, nv, nf, m);
-        if (st) return st;
+    S.nv = 0; S.hw = 0; S.nf = 0; S.kbase = 0; S.iters = 1; S.F1 = 4; S.unchanged = false;
+    // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN
+    const V3<T> f0 = uninml(s0, s1, s2), f1 = uninml(s0, s2, s3), f2 = uninml(s0, s1, s3), f3 = uninml(s1, s2, s3);
+    if (c.g.unib(is_zero_nml(f0) || is_zero_nml(f1) || is_zero_nml(f2) || is_zero_nml(f3)))
+        return GJKEPA_STATUS_DEGENERATE;
+    const T d0 = fabs(dot(vsub(O, s0), f0)), d1 = fabs(dot(vsub(O, s0), f1));
+    const T d2 = fabs(dot(vsub(O, s0), f2)), d3 = fabs(dot(vsub(O, s1), f3));
+    T minv = d0;
+    V3<T> dir = f0, a1 = s0;
+    if (d1 < minv) { minv = d1; dir = f1; a1 = s0; }
+    if (d2 < minv) { minv = d2; dir = f2; a1 = s0; }
+    if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
+    if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
+    T dt = dot(vsub(a1, O), dir);
+    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
+        // SUM over polytope(:,:,k), slot-major over faces: [s0 s0 s0 s1][s1 s2 s1 s2][s2 s3 s3 s3]
+        const T sx = ((((((((((s0.x + s0.x) + s0.x) + s1.x) + s1.x) + s2.x) + s1.x) + s2.x) + s2.x) + s3.x) + s3.x) + s3.x;
+        const T sy = ((((((((((s0.y + s0.y) + s0.y) + s1.y) + s1.y) + s2.y) + s1.y) + s2.y) + s2.y) + s3.y) + s3.y) + s3.y;
+        const T sz = ((((((((((s0.z + s0.z) + s0.z) + s1.z) + s1.z) + s2.z) + s1.z) + s2.z) + s2.z) + s3.z) + s3.z) + s3.z;
+        const T cnt = (T)12;
+        dt = dot(vsub(a1, vmk<T>(sx / cnt, sy / cnt, sz / cnt)), dir);
     }
-    int F1 = 4;
-    bool unchanged = false;
-    for (int iter = 1;; ++iter) {
-        // ---- end of iteration `iter`: MINLOC of the new polytope and the termination rules
-        const int F2 = nf;                                        // :956-969
-        face_argmin(c, F, minv, dir, a1);
-        V3<T> dir2 = dir;
-        if (c.g.unib(dot(vsub(a1, O), dir2) < T(0))) dir2 = vneg(dir2);
-        bool stop;                                                // :972-1015
-        if (F1 == F2) stop = unchanged || sorted_equal(c, F);    // unchanged hull: identical sorted lists
-        else stop = F1 > F2;
-        GK_STAMP(SE_TERM);
-        if (stop) { depth = minv; normal = dir2; return 0; }
-        // ---- iteration iter + 1: same faces as this iteration's F2, so its MINLOC carries over
-        iters = iter + 1;
-        if (iter + 1 > 99) return GJKEPA_STATUS_EPA_MAXITER;
-        F1 = nf;
-        T dt = dot(vsub(a1, O), dir);
-        if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(a1, polytope_centroid(c, F, F1)), dir);   // :905-908
-        if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
-        GK_STAMP(SE_DIR);
-        const V3<T> sp = support(c, dir);                          // :914
-        GK_STAMP(SE_SUP);
-        const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
-        if (two) {                        // net face count of two insertions unknown: save now
+    if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+    GK_STAMP(SE_IT1);
+    const V3<T> sp = support(c, dir);                          // :914
+    const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
+    // unique polytope vertices (getHullMeshesVertex, :920) + new point(s) -> ids 0..m-1
+    const bool u1 = !veq(s1, s0);
+    const bool u2 = !veq(s2, s0) && !veq(s2, s1);
+    const bool u3 = !veq(s3, s0) && !veq(s3, s1) && !veq(s3, s2);
+    const int i1 = 1, i2 = u1 ? 2 : 1, i3 = i2 + (u2 ? 1 : 0), isp = i3 + (u3 ? 1 : 0);
+    int m = isp + 1;
+    V3<T> sq = zero3<T>();
+    if (two) { sq = support(c, vneg(dir)); ++m; }
+    V3<T> q = s0;                                  // group lane j writes point j
+    bool w = gl == 0;
+    if (u1 && gl == i1) { q = s1; w = true; }
+    if (u2 && gl == i2) { q = s2; w = true; }
+    if (u3 && gl == i3) { q = s3; w = true; }
+    if (gl == isp) { q = sp; w = true; }
+    if (two && gl == isp + 1) { q = sq; w = true; }
+    if (w) { E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z; }
+    __builtin_amdgcn_wave_barrier();
+    GK_STAMP(SE_IT1);
+    return hull_build(c, S.F, S.kbase, S.hw, S.nv, S.nf, m);
+}
+
+// Closes iteration S.iters; if EPA goes on, runs the next iteration.  ST_CONT, 0 (depth and
+// normal set) or an error status / ST_DEFER.
+CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
+    constexpr int R = (FC + G - 1) / G;
+    auto& E = c.L.u.e;
+    const V3<T> O = zero3<T>();
+    const int gl = c.g.gl;
+    const int F2 = S.nf;                                      // :956-969
+    face_argmin(c, S.F, S.minv, S.dir, S.a1);
+    V3<T> dir2 = S.dir;
+    if (c.g.unib(dot(vsub(S.a1, O), dir2) < T(0))) dir2 = vneg(dir2);
+    bool stop;                                                // :972-1015
+    if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F);   // unchanged hull: identical sorted lists
+    else stop = S.F1 > F2;
+    GK_STAMP(SE_TERM);
+    if (stop) { depth = S.minv; normal = dir2; return 0; }
+    // ---- next iteration: same faces as this iteration's F2, so its MINLOC carries over
+    S.iters = S.iters + 1;
+    if (S.iters > 99) return GJKEPA_STATUS_EPA_MAXITER;
+    S.F1 = S.nf;
+    V3<T> dir = S.dir;
+    T dt = dot(vsub(S.a1, O), dir);
+    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(S.a1, polytope_centroid(c, S.F, S.F1)), dir);   // :905-908
+    if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+    GK_STAMP(SE_DIR);
+    const V3<T> sp = support(c, dir);                          // :914
+    GK_STAMP(SE_SUP);
+    const bool two = c.g.unib(fabs(S.minv) < Tol<T>::ZO);      // :935
+    if (two) {                            // net face count of two insertions unknown: save now
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int f = r * G + gl;
-                if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
-            }
+        for (int r = 0; r < R; ++r) {
+            const int f = r * G + gl;
+            if (f < FC) E.dsv[f] = (S.F.fv[r] & kEmpty) ? qnan<T>() : S.F.d[r];
         }
-        bool ch1 = false, ch2 = false;
-        int st = hull_add(c, F, kbase, hw, nv, nf, sp, true, 0, ch1, !two);
-        if (!st && two) st = hull_add(c, F, kbase, hw, nv, nf, support(c, vneg(dir)), true, 0, ch2, false);
-        unchanged = !ch1 && !ch2;
-        if (st) return st;
     }
+    bool ch1 = false, ch2 = false;
+    int st = hull_add(c, S.F, S.kbase, S.hw, S.nv, S.nf, sp, true, 0, ch1, !two);
+    if (!st && two) st = hull_add(c, S.F, S.kbase, S.hw, S.nv, S.nf, support(c, vneg(dir)), true, 0, ch2, false);
+    S.unchanged = !ch1 && !ch2;
+    return st ? st : ST_CONT;
+}
+
+CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf) {
+    EPAST_T S;
+    int st = epa_begin(c, S, s0, s1, s2, s3);
+    while (st == 0) {
+        st = epa_step(c, S, depth, normal);
+        if (st == ST_CONT) st = 0;
+        else break;
+    }
+    iters = S.iters;
+    nf = S.nf;
+    return st;
 }
 
 // ---------------------------------------------------------------- contact features
@@ -1639,6 +1663,133 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     GK_STAMP_END();
 }
 
+// Wave-uniform queue of the pairs routed to a launch, one 64-pair chunk at a time (first chunk
+// static, later ones from the launch counter as in for_each_routed_pair).
+struct PairQueue {
+    const uint8_t* route;
+    int64_t n_pairs, nchunks, ch, p0;
+    uint32_t* ctr;
+    uint32_t next;
+    uint64_t m;
+    int code;
+    bool done;
+    DEV void load_chunk() {
+        p0 = ch * 64;
+        const int64_t p = p0 + lane_id();
+        m = __ballot(p < n_pairs && (int)route[p] == code);
+    }
+    DEV PairQueue(const uint8_t* route_, int64_t n, int code_, uint32_t* ctr_)
+        : route(route_), n_pairs(n), nchunks((n + 63) / 64), ch(blockIdx.x), p0(0), ctr(ctr_), next(0), m(0),
+          code(code_), done(false) {
+        if (ch < nchunks) {
+            if (lane_id() == 0) next = gridDim.x + atomicAdd(ctr, 1u);
+            load_chunk();
+        } else {
+            done = true;
+        }
+    }
+    // next pair in order, -1 when the launch has no more
+    DEV int64_t pop() {
+        while (!m && !done) {
+            ch = (int64_t)__builtin_amdgcn_readfirstlane(next);
+            if (ch >= nchunks) { done = true; break; }
+            if (lane_id() == 0) next = gridDim.x + atomicAdd(ctr, 1u);
+            load_chunk();
+        }
+        if (!m) return -1;
+        const int bit = (int)__builtin_ctzll(m);
+        m &= m - 1;
+        return p0 + bit;
+    }
+};
+
+// EPA tier kernel with group refill: a group whose pair finished takes the next pair between
+// two EPA iterations (once at least REFILL groups of the wave are idle), so a wave no longer
+// runs every round to its slowest pair.  Results are the same as epa_kernel's.
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, int REFILL>
+__global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_args a) {
+    constexpr int R = (FC + G - 1) / G;
+    constexpr int NG = 64 / G;
+    using L_t = Lds<T, TIn, G, K, VC, FC>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<G> grp;
+    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    const int gl = grp.gl;
+    const int gid = grp.lane / G;
+    const TIn* verts = (const TIn*)a.verts;
+    PairQueue q(a.route, a.n_pairs, a.route_code, a.ctr);
+    Ctx<T, TIn, G, K, VC, FC> c{L, grp};
+    EpaState<T, R> S;
+    bool active = false;
+    int64_t pair = 0;
+    uint32_t gjk_it = 0;
+    // final record / park / route for a pair whose EPA ended with status r
+    auto finish = [&](int r, T depth, V3<T> n) {
+        uint32_t* slot = reinterpret_cast<uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
+        const uint32_t diag = (gjk_it & 0xffu) | ((uint32_t)(S.iters & 0xff) << 8) | ((uint32_t)(S.nf & 0xffff) << 16);
+        uint8_t next = 0;
+        if (r == ST_DEFER && a.next_code >= 0) {
+            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0));
+        } else if (r == 0) {
+            T* rec = reinterpret_cast<T*>(slot);
+            if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
+            if (gl == 4 % G) slot[sizeof(T) == 8 ? 27 : 14] = diag;
+            next = (uint8_t)(GJKEPA_ROUTE_CT0 + contact_tier_for(c.na > c.nb ? c.na : c.nb));
+        } else {
+            T o13[13];
+#pragma unroll
+            for (int i = 0; i < 13; ++i) o13[i] = T(0);
+            store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
+        }
+        if (gl == 0) a.route[pair] = next;
+    };
+    for (;;) {
+        // refill idle groups (in group order) once enough of them are idle
+        const uint64_t idle = __ballot(gl == 0 && !active);
+        const int nidle = popc(idle);
+        bool fresh = false;
+        if (!q.done && (nidle >= REFILL || nidle == NG)) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if ((idle >> (g * G)) & 1ull) {
+                    const int64_t p = q.pop();
+                    if (p >= 0 && gid == g) { pair = p; fresh = true; }
+                }
+            }
+        }
+        if (!__ballot(active || fresh)) break;
+        if (fresh) {
+            const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+            c.na = a.hull_cnt[ha];
+            c.nb = a.hull_cnt[hb];
+            const uint32_t* slot = reinterpret_cast<const uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
+            uint32_t kc[4];
+            kc[0] = slot[0]; kc[1] = slot[1]; kc[2] = slot[2]; kc[3] = slot[3];
+            gjk_it = slot[4];
+            load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+            S.iters = 1; S.nf = 0;
+            int r = ST_DEFER;
+            if (c.na <= G * K && c.nb <= G * K) {
+                const V3<T> s0 = decode_pt(c, kc[0]), s1 = decode_pt(c, kc[1]), s2 = decode_pt(c, kc[2]), s3 = decode_pt(c, kc[3]);
+                r = epa_begin(c, S, s0, s1, s2, s3);
+            }
+            __builtin_amdgcn_wave_barrier();
+            active = r == 0;
+            if (!active) finish(r, T(0), zero3<T>());
+        }
+        if (active) {
+            T depth = 0;
+            V3<T> n = zero3<T>();
+            const int r = epa_step(c, S, depth, n);
+            __builtin_amdgcn_wave_barrier();
+            if (r != ST_CONT) {
+                finish(r, depth, n);
+                active = false;
+            }
+        }
+    }
+}
+
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
 // finished, from the depth and normal it parked; writes the final record.
 template <typename TIn, typename T, int G, int K, int MINW>
@@ -1710,9 +1861,12 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, int REFILL = 0>
 hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
-    auto kfn = gk::epa_kernel<TIn, T, G, K, VC, FC, MINW>;
+    auto kfn = [] {
+        if constexpr (REFILL > 0) return gk::epa_kernel_refill<TIn, T, G, K, VC, FC, MINW, REFILL>;
+        else return gk::epa_kernel<TIn, T, G, K, VC, FC, MINW>;
+    }();
     constexpr int GPW = 64 / G;
     const size_t lds = sizeof(gk::Lds<T, TIn, G, K, VC, FC>) * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
@@ -1749,7 +1903,7 @@ hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
 template <typename TIn, typename T>
 hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
-        case 0: return launch_epa<TIn, T, EPA_ARGS(0)>(a, s);
+        case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
         case 1: return launch_epa<TIn, T, EPA_ARGS(1)>(a, s);
         case 2: return launch_epa<TIn, T, EPA_ARGS(2)>(a, s);
         default: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
