@@ -683,8 +683,9 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, V3<T>& a
 }
 
 // ALL(|sort(d1) - sort(d2)| < 1e-8), d1 = dsv[] (saved, NaN = no face), d2 = the current faces
-// (:972-1004).  Both lists hold n values.
-CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F) {
+// (:972-1004).  Both lists hold n values.  Slots at or above the high-water mark hw are empty now
+// and were when dsv[] was saved (hw never decreases), so the rank loops stop at hw.
+CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F, int hw) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
@@ -701,7 +702,7 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F) {
             const T x = E.x.s.cur[i];
             if (x == x) {
                 int rk = 0;
-                for (int j = 0; j < FC; ++j) { const T y = E.x.s.cur[j]; rk += (y < x) || (y == x && j < i); }
+                for (int j = 0; j < hw; ++j) { const T y = E.x.s.cur[j]; rk += (y < x) || (y == x && j < i); }
                 E.x.s.srt[rk] = x;
             }
         }
@@ -715,7 +716,7 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F) {
             const T x = E.dsv[i];
             if (x == x) {
                 int rk = 0;
-                for (int j = 0; j < FC; ++j) { const T y = E.dsv[j]; rk += (y < x) || (y == x && j < i); }
+                for (int j = 0; j < hw; ++j) { const T y = E.dsv[j]; rk += (y < x) || (y == x && j < i); }
                 if (!(fabs(x - E.x.s.srt[rk]) < Tol<T>::PT)) ok = false;
             }
         }
@@ -725,8 +726,9 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F) {
 }
 
 // SUM(polytope) / (3 F) over the face list in order (:905-908): faces sorted by key, then the
-// sequential sum over vertex slot j = 0..2 and face f (column-major polytope(F,3,3)).
-CTX_T DEV V3<T> polytope_centroid(CTX& c, const FACES_T& F, int nf) {
+// sequential sum over vertex slot j = 0..2 and face f (column-major polytope(F,3,3)).  Slots at or
+// above the high-water mark hw are empty.
+CTX_T DEV V3<T> polytope_centroid(CTX& c, const FACES_T& F, int nf, int hw) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
@@ -741,7 +743,7 @@ CTX_T DEV V3<T> polytope_centroid(CTX& c, const FACES_T& F, int nf) {
         const int f = r * G + gl;
         if (f < FC && !(F.fv[r] & kEmpty)) {
             int rk = 0;
-            for (int j = 0; j < FC; ++j) rk += E.x.o.key[j] < F.key[r];
+            for (int j = 0; j < hw; ++j) rk += E.x.o.key[j] < F.key[r];
             E.x.o.ord[rk] = F.fv[r];
         }
     }
@@ -843,7 +845,7 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     V3<T> dir2 = S.dir;
     if (c.g.unib(dot(vsub(S.a1, O), dir2) < T(0))) dir2 = vneg(dir2);
     bool stop;                                                // :972-1015
-    if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F);   // unchanged hull: identical sorted lists
+    if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F, S.hw);   // unchanged hull: identical sorted lists
     else stop = S.F1 > F2;
     GK_STAMP(SE_TERM);
     if (stop) { depth = S.minv; normal = dir2; return 0; }
@@ -853,7 +855,7 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     S.F1 = S.nf;
     V3<T> dir = S.dir;
     T dt = dot(vsub(S.a1, O), dir);
-    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(S.a1, polytope_centroid(c, S.F, S.F1)), dir);   // :905-908
+    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(S.a1, polytope_centroid(c, S.F, S.F1, S.hw)), dir);   // :905-908
     if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
     GK_STAMP(SE_DIR);
     const V3<T> sp = support(c, dir);                          // :914
@@ -1252,7 +1254,15 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
                 const TH* col = ax == 0 ? L.hx[h] : ax == 1 ? L.hy[h] : L.hz[h];
                 const int n = h ? c.nb : c.na;
                 T sum = 0;
-                for (int i = 0; i < n; ++i) sum += (T)col[i];
+                int i = 0;
+                for (; i + 8 <= n; i += 8) {         // loads batched ahead of the in-order adds
+                    TH v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = col[i + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sum += (T)v[u];
+                }
+                for (; i < n; ++i) sum += (T)col[i];
                 L.u.g.l1[j] = sum / (T)n;
             }
         }
@@ -1487,33 +1497,54 @@ DEV uint32_t match16(uint4 v, uint32_t code) {
     for (int i = 0; i < 16; ++i) m |= (((w[i >> 2] >> (8 * (i & 3))) & 0xffu) == code ? 1u : 0u) << i;
     return m;
 }
+// Work units of a launch (guided chunking): 64-pair chunks first, then the last `tail` pairs in
+// units of SMALL pairs, so a wave that takes its last unit late holds a few pairs, not 64.  The
+// tail covers about 64 pairs per workgroup of the grid (at most half the pairs).
+template <int SMALL> struct Units {
+    int64_t n_pairs, nbig, nunits;
+    DEV explicit Units(int64_t n) : n_pairs(n) {
+        int64_t tail = (int64_t)gridDim.x * 64;
+        if (tail > n / 2) tail = n / 2;
+        nbig = (n - tail) / 64;
+        nunits = nbig + (n - nbig * 64 + SMALL - 1) / SMALL;
+    }
+    DEV void range(int64_t u, int64_t& p0, int& len) const {
+        if (u < nbig) { p0 = u * 64; len = 64; }
+        else { p0 = nbig * 64 + (u - nbig) * SMALL; len = SMALL; }
+        if (p0 + len > n_pairs) len = (int)(n_pairs - p0);
+    }
+};
+
 template <int G, typename F>
 DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code,
                               uint32_t* ctr, int claim, F&& f) {
     // the first unit of workgroup b is unit b; later units come from the counter (offset by the
     // grid), so a launch with fewer units than workgroups issues no atomics at all
     const int64_t nchunks = (n_pairs + 63) / 64;
-    const int64_t nunits = claim <= 1 || route_code < 0 ? nchunks : (nchunks + 15) / 16;
     uint32_t next = 0;
-    if ((int64_t)blockIdx.x < nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
     if (claim <= 1 || route_code < 0) {
-        int64_t ch = blockIdx.x;
-        while (ch < nchunks) {
-            if (grp.lane == 0 && ch != (int64_t)blockIdx.x) next = gridDim.x + atomicAdd(ctr, 1u);   // prefetch
-            const int64_t p0 = ch * 64;
+        const Units<(64 / G > 8 ? 64 / G : 8)> U(n_pairs);
+        if ((int64_t)blockIdx.x < U.nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
+        int64_t u = blockIdx.x;
+        while (u < U.nunits) {
+            if (grp.lane == 0 && u != (int64_t)blockIdx.x) next = gridDim.x + atomicAdd(ctr, 1u);   // prefetch
+            int64_t p0;
+            int len;
+            U.range(u, p0, len);
             uint64_t m;
             if (route_code < 0) {
-                const int64_t left = n_pairs - p0;
-                m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+                m = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
             } else {
                 const int64_t p = p0 + grp.lane;
-                m = __ballot(p < n_pairs && (int)route[p] == route_code);
+                m = __ballot(grp.lane < len && (int)route[p] == route_code);
             }
             groups_take(grp, p0, m, f);
-            ch = (int64_t)__builtin_amdgcn_readfirstlane(next);
+            u = (int64_t)__builtin_amdgcn_readfirstlane(next);
         }
         return;
     }
+    const int64_t nunits = (nchunks + 15) / 16;
+    if ((int64_t)blockIdx.x < nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
     // runs of 16 chunks: lane l loads route bytes [16 l, 16 l + 16) of the run in one 16-byte load
     for (int64_t run = blockIdx.x; run * 16 < nchunks; run = (int64_t)__builtin_amdgcn_readfirstlane(next)) {
         if (grp.lane == 0 && run != (int64_t)blockIdx.x) next = gridDim.x + atomicAdd(ctr, 1u);
@@ -1663,25 +1694,26 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     GK_STAMP_END();
 }
 
-// Wave-uniform queue of the pairs routed to a launch, one 64-pair chunk at a time (first chunk
+// Wave-uniform queue of the pairs routed to a launch, one work unit at a time (first unit
 // static, later ones from the launch counter as in for_each_routed_pair).
-struct PairQueue {
+template <int SMALL> struct PairQueue {
     const uint8_t* route;
-    int64_t n_pairs, nchunks, ch, p0;
+    Units<SMALL> U;
+    int64_t ch, p0;
     uint32_t* ctr;
     uint32_t next;
     uint64_t m;
     int code;
     bool done;
     DEV void load_chunk() {
-        p0 = ch * 64;
+        int len;
+        U.range(ch, p0, len);
         const int64_t p = p0 + lane_id();
-        m = __ballot(p < n_pairs && (int)route[p] == code);
+        m = __ballot(lane_id() < len && (int)route[p] == code);
     }
     DEV PairQueue(const uint8_t* route_, int64_t n, int code_, uint32_t* ctr_)
-        : route(route_), n_pairs(n), nchunks((n + 63) / 64), ch(blockIdx.x), p0(0), ctr(ctr_), next(0), m(0),
-          code(code_), done(false) {
-        if (ch < nchunks) {
+        : route(route_), U(n), ch(blockIdx.x), p0(0), ctr(ctr_), next(0), m(0), code(code_), done(false) {
+        if (ch < U.nunits) {
             if (lane_id() == 0) next = gridDim.x + atomicAdd(ctr, 1u);
             load_chunk();
         } else {
@@ -1692,7 +1724,7 @@ struct PairQueue {
     DEV int64_t pop() {
         while (!m && !done) {
             ch = (int64_t)__builtin_amdgcn_readfirstlane(next);
-            if (ch >= nchunks) { done = true; break; }
+            if (ch >= U.nunits) { done = true; break; }
             if (lane_id() == 0) next = gridDim.x + atomicAdd(ctr, 1u);
             load_chunk();
         }
@@ -1717,7 +1749,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     const int gl = grp.gl;
     const int gid = grp.lane / G;
     const TIn* verts = (const TIn*)a.verts;
-    PairQueue q(a.route, a.n_pairs, a.route_code, a.ctr);
+    PairQueue<(2 * NG > 8 ? 2 * NG : 8)> q(a.route, a.n_pairs, a.route_code, a.ctr);
     Ctx<T, TIn, G, K, VC, FC> c{L, grp};
     EpaState<T, R> S;
     bool active = false;
