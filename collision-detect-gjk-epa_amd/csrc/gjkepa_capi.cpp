@@ -4,7 +4,8 @@
 // needed and are reused; they are serialised per device by a mutex, so concurrent callers (the
 // reference's `!$OMP PARALLEL DO ... CALL GJKEPA` pattern) are safe.  gjkepa_batch_device never
 // allocates or synchronises: it enqueues a 64-byte counter reset and eight kernels (2 GJK + 4 EPA +
-// 2 contact tiers); each kernel takes 64-pair chunks from its own counter.
+// 2 contact tiers); each kernel takes 64-pair chunks from its own counter.  gjkepa_hull_batch(_device)
+// follow the same pattern for the batched convex-hull kernels (two tiers over one cloud list).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -15,6 +16,7 @@
 
 #include "../../include/gjkepa.h"
 #include "gjkepa_kernel.h"
+#include "hull_kernel.h"
 
 namespace {
 
@@ -52,6 +54,7 @@ struct DeviceState {
     int num_cus = 0;
     hipStream_t stream = nullptr;
     DevBuf verts, off, cnt, pairs, out, ws;
+    DevBuf h_foff, h_faces, h_nf, h_nv, h_st, h_hv, h_vi;   // gjkepa_hull_batch staging
 };
 
 std::mutex g_table_mu;
@@ -134,6 +137,19 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     return 0;
 }
 
+// select `device` and create its stream on first use (caller holds d->mu)
+int init_device(DeviceState* d, int device) {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (!d->init) {
+        e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        d->num_cus = num_cus_current();
+        d->init = true;
+    }
+    return 0;
+}
+
 bool valid_enums(int32_t vert_dtype, int32_t precision) {
     return (vert_dtype == GJKEPA_DTYPE_F32 || vert_dtype == GJKEPA_DTYPE_F64) &&
            (precision == GJKEPA_PREC_F32 || precision == GJKEPA_PREC_F64);
@@ -202,14 +218,8 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
     DeviceState* d = device_state(device, &rc);
     if (!d) return rc;
     std::lock_guard<std::mutex> g(d->mu);
-    hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    if (!d->init) {
-        e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
-        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-        d->num_cus = num_cus_current();
-        d->init = true;
-    }
+    if ((rc = init_device(d, device))) return rc;
+    hipError_t e;
     const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
     const size_t rec = (size_t)gjkepa_record_bytes(precision);
     if ((e = d->verts.ensure((size_t)n_vert_scalars * esz)) != hipSuccess ||
@@ -263,6 +273,106 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     }
     *penetration_depth = r.penetration_depth;
     if (status) *status = r.status;
+    return 0;
+}
+
+// ---- batched convex hulls (include/gjkepa.h) ------------------------------
+int64_t gjkepa_hull_face_capacity(int32_t n_points) { return n_points >= 4 ? 2 * (int64_t)n_points - 4 : 0; }
+
+int gjkepa_hull_batch_device(int32_t vert_dtype, const void* points, const int64_t* cloud_off,
+                             const int32_t* cloud_cnt, int64_t n_clouds, const int64_t* face_off,
+                             int32_t* faces, int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                             void* hull_verts, int32_t* vert_idx, void* stream) {
+    if (n_clouds < 0 || (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64))
+        return fail(GJKEPA_E_ARG, "bad n_clouds/dtype");
+    if (n_clouds == 0) return 0;
+    if (!points || !cloud_off || !cloud_cnt || !face_off || !faces || !n_faces || !n_verts || !status)
+        return fail(GJKEPA_E_ARG, "null pointer");
+    gjkepa_hull_args a{};
+    a.points = points;
+    a.cloud_off = cloud_off;
+    a.cloud_cnt = cloud_cnt;
+    a.n_clouds = n_clouds;
+    a.face_off = face_off;
+    a.faces = faces;
+    a.n_faces = n_faces;
+    a.n_verts = n_verts;
+    a.status = status;
+    a.hull_verts = hull_verts;
+    a.vert_idx = vert_idx;
+    a.num_cus = num_cus_current();
+    hipError_t e = gjkepa_launch_hull(vert_dtype, a, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "hull kernel launch");
+}
+
+int gjkepa_hull_batch(int32_t vert_dtype, const void* points, int64_t n_point_scalars,
+                      const int64_t* cloud_off, const int32_t* cloud_cnt, int64_t n_clouds,
+                      const int64_t* face_off, int64_t n_face_slots, int32_t* faces,
+                      int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                      void* hull_verts, int32_t* vert_idx, int32_t device) {
+    if (n_clouds < 0 || n_point_scalars < 0 || n_face_slots < 0 ||
+        (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64))
+        return fail(GJKEPA_E_ARG, "bad sizes/dtype");
+    if (n_clouds == 0) return 0;
+    if (!points || !cloud_off || !cloud_cnt || !face_off || !faces || !n_faces || !n_verts || !status)
+        return fail(GJKEPA_E_ARG, "null pointer");
+    // host-side validation of the index structure (device code trusts it)
+    for (int64_t c = 0; c < n_clouds; ++c) {
+        const int64_t n = cloud_cnt[c];
+        if (n < 4 || n > GJKEPA_HULL_MAX_POINTS) continue;      // answered with BAD_INPUT, nothing read
+        if (cloud_off[c] < 0 || cloud_off[c] + 3 * n > n_point_scalars) return fail(GJKEPA_E_ARG, "cloud outside the point pool");
+        if (face_off[c] < 0 || face_off[c] + gjkepa_hull_face_capacity((int32_t)n) > n_face_slots)
+            return fail(GJKEPA_E_ARG, "cloud's face block outside the face buffer");
+    }
+    int rc = 0;
+    DeviceState* d = device_state(device, &rc);
+    if (!d) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    if ((rc = init_device(d, device))) return rc;
+    const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
+    const size_t pb = (size_t)n_point_scalars * esz, nc = (size_t)n_clouds;
+    hipError_t e;
+    if ((e = d->verts.ensure(pb)) != hipSuccess || (e = d->off.ensure(nc * 8)) != hipSuccess ||
+        (e = d->cnt.ensure(nc * 4)) != hipSuccess || (e = d->h_foff.ensure(nc * 8)) != hipSuccess ||
+        (e = d->h_faces.ensure((size_t)n_face_slots * 12 + 12)) != hipSuccess ||
+        (e = d->h_nf.ensure(nc * 4)) != hipSuccess || (e = d->h_nv.ensure(nc * 4)) != hipSuccess ||
+        (e = d->h_st.ensure(nc)) != hipSuccess ||
+        (hull_verts && (e = d->h_hv.ensure(pb)) != hipSuccess) ||
+        (vert_idx && (e = d->h_vi.ensure((size_t)n_point_scalars * 4)) != hipSuccess))
+        return hip_fail(e, "hipMalloc");
+    hipStream_t s = d->stream;
+    if ((e = hipMemcpyAsync(d->verts.p, points, pb, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->off.p, cloud_off, nc * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->cnt.p, cloud_cnt, nc * 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->h_foff.p, face_off, nc * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    rc = gjkepa_hull_batch_device(vert_dtype, d->verts.p, (const int64_t*)d->off.p, (const int32_t*)d->cnt.p,
+                                  n_clouds, (const int64_t*)d->h_foff.p, (int32_t*)d->h_faces.p,
+                                  (int32_t*)d->h_nf.p, (int32_t*)d->h_nv.p, (int8_t*)d->h_st.p,
+                                  hull_verts ? d->h_hv.p : nullptr, vert_idx ? (int32_t*)d->h_vi.p : nullptr, s);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(n_faces, d->h_nf.p, nc * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(n_verts, d->h_nv.p, nc * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(status, d->h_st.p, nc, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    // copy back only the written parts: each cloud's faces, hull vertices and vertex indices
+    std::vector<int32_t> hf((size_t)n_face_slots * 3);
+    std::vector<unsigned char> hh(hull_verts ? pb : 0);
+    std::vector<int32_t> hi(vert_idx ? (size_t)n_point_scalars : 0);
+    if ((e = hipMemcpyAsync(hf.data(), d->h_faces.p, hf.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (hull_verts && (e = hipMemcpyAsync(hh.data(), d->h_hv.p, pb, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+        (vert_idx && (e = hipMemcpyAsync(hi.data(), d->h_vi.p, hi.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    for (int64_t c = 0; c < n_clouds; ++c) {
+        const int64_t nf = n_faces[c], nv = n_verts[c];
+        if (nf) std::memcpy(faces + 3 * face_off[c], hf.data() + 3 * face_off[c], (size_t)nf * 12);
+        if (nv && hull_verts)
+            std::memcpy((unsigned char*)hull_verts + (size_t)cloud_off[c] * esz, hh.data() + (size_t)cloud_off[c] * esz,
+                        (size_t)(3 * nv) * esz);
+        if (nv && vert_idx) std::memcpy(vert_idx + cloud_off[c], hi.data() + cloud_off[c], (size_t)nv * 4);
+    }
     return 0;
 }
 

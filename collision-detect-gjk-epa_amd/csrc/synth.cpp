@@ -96,3 +96,47 @@ extern "C" int64_t gjkepa_synth_pairs(uint64_t seed, int64_t first_pair, int64_t
     }
     return total;
 }
+
+// Point clouds for the batched hull module: cloud c has n ~ U{n_min..n_max}
+// points, uniform in the unit ball (shape 0: mostly interior points, a raw scan-like cloud) or on
+// the unit sphere (shape 1: every point extreme, the hull's worst case).  Same counter-based
+// streams as the pairs (keyed by the global cloud index), coordinates rounded to fp32.
+extern "C" int64_t gjkepa_synth_clouds(uint64_t seed, int64_t first_cloud, int64_t n_clouds,
+                                       int32_t n_min, int32_t n_max, int32_t shape,
+                                       int32_t vert_dtype, void* verts,
+                                       int64_t* cloud_off, int32_t* cloud_cnt) {
+    if (n_clouds < 0 || n_min < 1 || n_max < n_min || n_max > GJKEPA_HULL_MAX_POINTS || (shape != 0 && shape != 1))
+        return GJKEPA_E_ARG;
+    if (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64) return GJKEPA_E_ARG;
+    std::vector<int32_t> cnt((size_t)n_clouds);
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < n_clouds; ++c) {
+        PairRng g(seed ^ 0xC10D5ull, first_cloud + c);
+        cnt[c] = draw_n(g, n_min, n_max);
+    }
+    std::vector<int64_t> off((size_t)n_clouds + 1);
+    off[0] = 0;
+    for (int64_t c = 0; c < n_clouds; ++c) off[c + 1] = off[c] + 3 * (int64_t)cnt[c];
+    const int64_t total = off[n_clouds];
+    if (!verts) return total;
+    if (!cloud_off || !cloud_cnt) return GJKEPA_E_ARG;
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < n_clouds; ++c) {
+        PairRng g(seed ^ 0xC10D5ull, first_cloud + c);
+        const int32_t n = draw_n(g, n_min, n_max);
+        const int64_t o = off[c];
+        for (int32_t i = 0; i < n; ++i) {
+            double v[3];
+            unit_vec(g, v);
+            const double r = shape == 0 ? std::cbrt(g.u01()) : 1.0;
+            for (int d = 0; d < 3; ++d) {
+                const float val = (float)(v[d] * r);
+                if (vert_dtype == GJKEPA_DTYPE_F32) ((float*)verts)[o + (int64_t)d * n + i] = val;
+                else ((double*)verts)[o + (int64_t)d * n + i] = (double)val;
+            }
+        }
+        cloud_off[c] = o;
+        cloud_cnt[c] = n;
+    }
+    return total;
+}

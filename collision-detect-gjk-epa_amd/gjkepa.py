@@ -30,7 +30,9 @@ MAX_HULL_VERTS = 256
 EXPORTS = (
     "gjkepa_record_bytes", "gjkepa_query", "gjkepa_batch", "gjkepa_workspace_bytes",
     "gjkepa_batch_device", "gjkepa_last_error", "gjkepa_version_string", "gjkepa_synth_pairs",
+    "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
 )
+HULL_MAX_POINTS = 256
 
 REC64 = np.dtype([
     ("penetration_depth", "<f8"), ("collision_normal", "<f8", (3,)), ("collision_point", "<f8", (3,)),
@@ -62,6 +64,13 @@ def load(path: str | None = None) -> ctypes.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = path or os.environ.get("GJKEPA_LIB") or LIB_PATH
+    try:
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 (same soname as
+        # /opt/rocm's).  Whichever loads first serves both, and torch's device init fails when it
+        # finds the system runtime already mapped, so bring torch's in first when torch is present.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise GjkEpaError(f"{p} not built; run `make -C collision-detect-gjk-epa_amd`")
     lib = ctypes.CDLL(p)
@@ -80,6 +89,16 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_batch_device.restype = ctypes.c_int
     lib.gjkepa_synth_pairs.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp, c_vp]
     lib.gjkepa_synth_pairs.restype = c_i64
+    lib.gjkepa_hull_face_capacity.argtypes = [c_i32]
+    lib.gjkepa_hull_face_capacity.restype = c_i64
+    lib.gjkepa_hull_batch.argtypes = [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_i32]
+    lib.gjkepa_hull_batch.restype = ctypes.c_int
+    lib.gjkepa_hull_batch_device.argtypes = [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                             c_vp]
+    lib.gjkepa_hull_batch_device.restype = ctypes.c_int
+    lib.gjkepa_synth_clouds.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]
+    lib.gjkepa_synth_clouds.restype = c_i64
     if path is None:
         _lib = lib
     return lib
@@ -214,3 +233,113 @@ def gjkepa_batch_device(version: int, tol_ff: float, vert_dtype: int, precision:
 
 def version_string() -> str:
     return load().gjkepa_version_string().decode()
+
+
+# ---- batched convex hulls (include/gjkepa.h gjkepa_hull_batch) ----------------
+@dataclass
+class CloudPool:
+    """Pooled point clouds: cloud c = verts[off[c] : off[c] + 3*cnt[c]] as x[], y[], z[]."""
+    verts: np.ndarray      # float32 or float64
+    cloud_off: np.ndarray  # int64
+    cloud_cnt: np.ndarray  # int32
+
+    @property
+    def n_clouds(self) -> int:
+        return int(self.cloud_cnt.shape[0])
+
+    @property
+    def dtype_code(self) -> int:
+        return DTYPE_F32 if self.verts.dtype == np.float32 else DTYPE_F64
+
+    def cloud(self, c: int) -> np.ndarray:
+        o, n = int(self.cloud_off[c]), int(self.cloud_cnt[c])
+        return self.verts[o:o + 3 * n].reshape(3, n).T.astype(np.float64)
+
+    @staticmethod
+    def from_list(clouds, dtype=np.float64) -> "CloudPool":
+        chunks, off, cnt, o = [], [], [], 0
+        for p in clouds:
+            p = np.asarray(p, dtype=np.float64).reshape(-1, 3)
+            chunks.append(p.T.reshape(-1))
+            off.append(o)
+            cnt.append(p.shape[0])
+            o += 3 * p.shape[0]
+        verts = np.concatenate(chunks).astype(dtype) if chunks else np.zeros(0, dtype)
+        return CloudPool(verts, np.asarray(off, np.int64), np.asarray(cnt, np.int32))
+
+
+def hull_face_offsets(cloud_cnt) -> np.ndarray:
+    """Triangle offset of each cloud's face block (exclusive prefix sum of 2n - 4, 0 for n < 4)."""
+    cnt = np.asarray(cloud_cnt, np.int64)
+    cap = np.where(cnt >= 4, 2 * cnt - 4, 0)
+    off = np.zeros(len(cap), np.int64)
+    if len(cap) > 1:
+        off[1:] = np.cumsum(cap)[:-1]
+    return off
+
+
+def synth_clouds(seed: int, n_clouds: int, n_min: int = 64, n_max: int = 64, shape: int = 0,
+                 first_cloud: int = 0, dtype=np.float32) -> CloudPool:
+    """Deterministic synthetic clouds: uniform in the unit ball (shape 0) or on the sphere (shape 1)."""
+    lib = load()
+    code = DTYPE_F32 if np.dtype(dtype) == np.float32 else DTYPE_F64
+    total = lib.gjkepa_synth_clouds(seed, first_cloud, n_clouds, n_min, n_max, shape, code, None, None, None)
+    if total < 0:
+        raise GjkEpaError("gjkepa_synth_clouds: bad arguments")
+    verts = np.empty(total, dtype=dtype)
+    off = np.empty(n_clouds, np.int64)
+    cnt = np.empty(n_clouds, np.int32)
+    lib.gjkepa_synth_clouds(seed, first_cloud, n_clouds, n_min, n_max, shape, code, _ptr(verts), _ptr(off), _ptr(cnt))
+    return CloudPool(verts, off, cnt)
+
+
+def hull_batch(pool: CloudPool, device: int = 0) -> dict:
+    """Convex hull of every cloud on the GPU (host buffers, blocking).  Returns faces (int32
+    [sum(2n-4), 3], cloud c's n_faces[c] triangles at face_off[c]), face_off, n_faces, n_verts,
+    status, hull_verts (pool layout: cloud c's hull at cloud_off[c], stride n_verts[c]) and
+    vert_idx (cloud c's hull vertex indices at cloud_off[c])."""
+    lib = load()
+    verts = np.ascontiguousarray(pool.verts)
+    off = np.ascontiguousarray(pool.cloud_off, np.int64)
+    cnt = np.ascontiguousarray(pool.cloud_cnt, np.int32)
+    n = cnt.size
+    foff = hull_face_offsets(cnt)
+    nslots = int(foff[-1] + max(2 * int(cnt[-1]) - 4, 0)) if n else 0
+    faces = np.full((max(nslots, 1), 3), -1, np.int32)
+    nf = np.zeros(n, np.int32)
+    nv = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int8)
+    hv = np.zeros_like(verts)
+    vi = np.full(verts.size, -1, np.int32)
+    rc = lib.gjkepa_hull_batch(pool.dtype_code, _ptr(verts), verts.size, _ptr(off), _ptr(cnt), n, _ptr(foff), nslots,
+                               _ptr(faces), _ptr(nf), _ptr(nv), _ptr(st), _ptr(hv), _ptr(vi), int(device))
+    _check(rc, "gjkepa_hull_batch")
+    return dict(faces=faces[:nslots], face_off=foff, n_faces=nf, n_verts=nv, status=st, hull_verts=hv, vert_idx=vi)
+
+
+def hull_batch_device(vert_dtype: int, points_ptr: int, cloud_off_ptr: int, cloud_cnt_ptr: int, n_clouds: int,
+                      face_off_ptr: int, faces_ptr: int, n_faces_ptr: int, n_verts_ptr: int, status_ptr: int,
+                      hull_verts_ptr: int = 0, vert_idx_ptr: int = 0, stream: int = 0) -> None:
+    """Device-resident hull batch (raw device pointers), asynchronous on `stream`."""
+    rc = load().gjkepa_hull_batch_device(int(vert_dtype), points_ptr, cloud_off_ptr, cloud_cnt_ptr, int(n_clouds),
+                                         face_off_ptr, faces_ptr, n_faces_ptr, n_verts_ptr, status_ptr,
+                                         hull_verts_ptr or None, vert_idx_ptr or None, stream or None)
+    _check(rc, "gjkepa_hull_batch_device")
+
+
+def quickhull(points, device: int = 0):
+    """GCLIB_QuickHull::QuickHull(points, polytope, info) as called at GCLIB_GJKEPA.f90:950:
+    the hull of an (n, 3) cloud as a triangle soup polytope(F, 3, 3) (face, vertex, xyz), outward
+    wound; info = the GJKEPA_STATUS_* code (0 = OK)."""
+    p = np.asarray(points, np.float64).reshape(-1, 3)
+    r = hull_batch(CloudPool.from_list([p]), device)
+    nf = int(r["n_faces"][0])
+    return p[r["faces"][:nf]], int(r["status"][0])
+
+
+def hull_mesh_vertices(polytope) -> np.ndarray:
+    """GCLIB_DeHull::getHullMeshesVertex(polytope, points, info) (GCLIB_GJKEPA.f90:920): the
+    distinct vertices of a triangle soup, in order of first appearance (host-side; exact equality)."""
+    v = np.asarray(polytope, np.float64).reshape(-1, 3)
+    _, first = np.unique(v, axis=0, return_index=True)
+    return v[np.sort(first)]

@@ -138,6 +138,60 @@ int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int3
                         void* out, void* workspace, int64_t workspace_bytes,
                         void* stream);
 
+/* ---- batched convex hulls ----------------------------------------------
+ * The reference rebuilds a convex hull every EPA iteration with
+ *   CALL QuickHull(scatPoints, polytope_2_, info)           (GCLIB_GJKEPA.f90:950)
+ *   CALL getHullMeshesVertex(polytope_1_, scatPoints, info) (GCLIB_GJKEPA.f90:920)
+ * from the unvendored modules GCLIB_QuickHull / GCLIB_DeHull (:14-15, no version pin).  These
+ * entries expose the same two operations as a first-class batched device module: the hull of
+ * every point cloud of a pool as outward triangles (QuickHull) plus the hull's vertex set
+ * (getHullMeshesVertex), so callers can reduce raw point clouds to hulls before the narrow phase.
+ *
+ * Algorithm (restated bit for bit by oracle/gjkepa_oracle.c: oracle_hull_batch): QuickHull with a
+ * global furthest-point order, fp64 arithmetic, absolute epsilon GJKEPA_HULL_EPS.
+ *   1. initial tetrahedron: i0 = first argmin x; i1 = first argmax |p - p_i0|^2;
+ *      i2 = first argmax |(p_i1 - p_i0) x (p - p_i0)|^2; i3 = first argmax |(p - p_i0).n|,
+ *      n = (p_i1 - p_i0) x (p_i2 - p_i0).  Collinear / coplanar / coincident clouds (distance
+ *      <= eps at any step) are GJKEPA_STATUS_DEGENERATE.
+ *   2. every other point is assigned to the face it is furthest above (first face on ties) when
+ *      that distance exceeds eps, otherwise discarded as interior.
+ *   3. repeat: the eye is the assigned point furthest above its face (lowest index on ties); every
+ *      face the eye is more than eps above is removed; each horizon edge (u, w) is coned to the
+ *      eye as face (u, w, eye); points of removed faces are re-assigned among the new faces only.
+ * Face slots: new faces take the removed faces' slots in slot order, then append; faces are
+ * reported in slot order.  Outward winding: normal = (b - a) x (c - b) points out of the hull.
+ * Vertex set (getHullMeshesVertex): the points the faces reference, in ascending point index.
+ *
+ * Layout.  Input clouds use the hull-pool layout above (cloud c: cloud_cnt[c] points, SoA at
+ * scalar offset cloud_off[c]).  Cloud c's faces are written as int32 (a, b, c) point-index
+ * triples at triangle offset face_off[c] of `faces`, with room for gjkepa_hull_face_capacity(
+ * cloud_cnt[c]) = 2n - 4 triangles.  Optional outputs (NULL to skip), both at cloud_off[c]:
+ * `hull_verts` (same dtype as the input) receives the hull as a pool entry of n_verts[c] points,
+ * SoA with stride n_verts[c], directly usable as a gjkepa_batch hull with hull_cnt = n_verts;
+ * `vert_idx` (int32) receives the hull vertices' point indices.
+ * status[c]: GJKEPA_STATUS_OK, _DEGENERATE (flat cloud, zero-area cone face or a non-manifold
+ * horizon that overflows 2n - 4 face slots) or _BAD_INPUT (n < 4, n > GJKEPA_HULL_MAX_POINTS,
+ * non-finite coordinates); n_faces = n_verts = 0 unless OK. */
+#define GJKEPA_HULL_MAX_POINTS 256
+#define GJKEPA_HULL_EPS 1.0e-10
+
+/* Triangle slots cloud c needs in `faces`: 2n - 4 (0 for n < 4). */
+int64_t gjkepa_hull_face_capacity(int32_t n_points);
+
+/* Host buffers, blocking.  n_point_scalars / n_face_slots bound the pool and face buffers. */
+int gjkepa_hull_batch(int32_t vert_dtype, const void* points, int64_t n_point_scalars,
+                      const int64_t* cloud_off, const int32_t* cloud_cnt, int64_t n_clouds,
+                      const int64_t* face_off, int64_t n_face_slots, int32_t* faces,
+                      int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                      void* hull_verts, int32_t* vert_idx, int32_t device);
+
+/* Device buffers, asynchronous on `stream` (hipStream_t or NULL); no allocation, no sync. */
+int gjkepa_hull_batch_device(int32_t vert_dtype, const void* points,
+                             const int64_t* cloud_off, const int32_t* cloud_cnt, int64_t n_clouds,
+                             const int64_t* face_off, int32_t* faces,
+                             int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                             void* hull_verts, int32_t* vert_idx, void* stream);
+
 /* Last error message of the calling thread ("" if none). */
 const char* gjkepa_last_error(void);
 
@@ -157,6 +211,14 @@ int64_t gjkepa_synth_pairs(uint64_t seed, int64_t first_pair, int64_t n_pairs,
                            int32_t n_min, int32_t n_max, double r_max,
                            int32_t vert_dtype, void* verts,
                            int64_t* hull_off, int32_t* hull_cnt, int32_t* pairs);
+
+/* Synthetic point clouds for the hull module: n ~ U{n_min..n_max} points per cloud, uniform in the
+ * unit ball (shape 0) or on the unit sphere (shape 1); same conventions as gjkepa_synth_pairs
+ * (counter-based per global cloud index, fp32-rounded; verts == NULL returns the scalar count). */
+int64_t gjkepa_synth_clouds(uint64_t seed, int64_t first_cloud, int64_t n_clouds,
+                            int32_t n_min, int32_t n_max, int32_t shape,
+                            int32_t vert_dtype, void* verts,
+                            int64_t* cloud_off, int32_t* cloud_cnt);
 
 #ifdef __cplusplus
 }

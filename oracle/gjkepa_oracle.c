@@ -774,3 +774,186 @@ int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
     }
     return 0;
 }
+
+/* ==== batched convex hulls ==============================================
+ * GCLIB_QuickHull::QuickHull + GCLIB_DeHull::getHullMeshesVertex as used at GCLIB_GJKEPA.f90:920,
+ * :950 (unvendored, no version pin), with the algorithm fixed in include/gjkepa.h: QuickHull in
+ * global furthest-point order, fp64, absolute epsilon GJKEPA_HULL_EPS, new faces in the removed
+ * faces' slots (slot order) then appended.  hull_kernel.hip follows this operation for operation. */
+#define QH_FCAP (2 * GJKEPA_HULL_MAX_POINTS - 4)
+typedef struct {
+    v3 p[GJKEPA_HULL_MAX_POINTS];
+    int st[GJKEPA_HULL_MAX_POINTS];       /* assigned face slot, -1 = interior / processed */
+    double dist[GJKEPA_HULL_MAX_POINTS];  /* distance above the assigned face */
+    int fv[QH_FCAP][3];                   /* face vertex ids; fv[f][0] < 0: dead slot */
+    v3 fn[QH_FCAP];                       /* UNINML of the stored (outward) order */
+    int vis[QH_FCAP], vl[QH_FCAP], hu[QH_FCAP], hw[QH_FCAP], ns[QH_FCAP];
+    unsigned char used[GJKEPA_HULL_MAX_POINTS];
+} qhbuf;
+
+/* signed distance of p above face f (the DIST_PF_SIGN recipe, :1357-1377) */
+static inline double qh_dist(const qhbuf* Q, int f, v3 p) { return dot(vsub(p, Q->p[Q->fv[f][0]]), Q->fn[f]); }
+
+static int qh_cloud(qhbuf* Q, int n, int32_t* faces, int32_t* nf_out, int32_t* vidx, int32_t* nv_out) {
+    const double eps = GJKEPA_HULL_EPS;
+    const int fcap = 2 * n - 4;
+    *nf_out = 0; *nv_out = 0;
+    for (int j = 0; j < n; ++j)
+        if (!isfinite(Q->p[j].x) || !isfinite(Q->p[j].y) || !isfinite(Q->p[j].z)) return GJKEPA_STATUS_BAD_INPUT;
+    /* 1. initial tetrahedron */
+    int i0 = 0;
+    for (int j = 1; j < n; ++j) if (Q->p[j].x < Q->p[i0].x) i0 = j;
+    v3 p0 = Q->p[i0];
+    int i1 = 0; double b = -1.0;
+    for (int j = 0; j < n; ++j) { v3 d = vsub(Q->p[j], p0); double v = dot(d, d); if (v > b) { b = v; i1 = j; } }
+    v3 e1 = vsub(Q->p[i1], p0);
+    double l1 = norm2(e1);
+    if (!(l1 > eps)) return GJKEPA_STATUS_DEGENERATE;
+    int i2 = 0; b = -1.0;
+    for (int j = 0; j < n; ++j) { v3 c = cross(e1, vsub(Q->p[j], p0)); double v = dot(c, c); if (v > b) { b = v; i2 = j; } }
+    v3 pn = cross(e1, vsub(Q->p[i2], p0));
+    double lp = norm2(pn);
+    if (!(lp / l1 > eps)) return GJKEPA_STATUS_DEGENERATE;
+    int i3 = 0; b = -1.0;
+    for (int j = 0; j < n; ++j) { double v = fabs(dot(vsub(Q->p[j], p0), pn)); if (v > b) { b = v; i3 = j; } }
+    if (!(b / lp > eps)) return GJKEPA_STATUS_DEGENERATE;
+    const int t[4] = {i0, i1, i2, i3};
+    v3 T[4] = {Q->p[i0], Q->p[i1], Q->p[i2], Q->p[i3]};
+    v3 cen = centroid4(T);
+    static const int SEED[4][3] = {{0, 1, 2}, {0, 2, 3}, {0, 1, 3}, {1, 2, 3}};
+    for (int f = 0; f < 4; ++f) {
+        int a = t[SEED[f][0]], bb = t[SEED[f][1]], c = t[SEED[f][2]];
+        v3 nn = cross(vsub(Q->p[bb], Q->p[a]), vsub(Q->p[c], Q->p[bb]));
+        if (dot(nn, vsub(Q->p[a], cen)) < 0.0) { int s = bb; bb = c; c = s; }
+        Q->fv[f][0] = a; Q->fv[f][1] = bb; Q->fv[f][2] = c;
+        Q->fn[f] = uninml(Q->p[a], Q->p[bb], Q->p[c]);
+        if (is_zero_nml(Q->fn[f])) return GJKEPA_STATUS_DEGENERATE;
+        Q->vis[f] = 0;
+    }
+    int hwm = 4;
+    /* 2. initial assignment */
+    for (int j = 0; j < n; ++j) {
+        Q->st[j] = -1;
+        if (j == i0 || j == i1 || j == i2 || j == i3) continue;
+        double best = -DBL_MAX; int bf = -1;
+        for (int f = 0; f < 4; ++f) { double d = qh_dist(Q, f, Q->p[j]); if (d > best) { best = d; bf = f; } }
+        if (best > eps) { Q->st[j] = bf; Q->dist[j] = best; }
+    }
+    /* 3. furthest-point expansion */
+    for (;;) {
+        int eye = -1; double be = -DBL_MAX;
+        for (int j = 0; j < n; ++j) if (Q->st[j] >= 0 && Q->dist[j] > be) { be = Q->dist[j]; eye = j; }
+        if (eye < 0) break;
+        v3 pe = Q->p[eye];
+        int nvis = 0;
+        for (int f = 0; f < hwm; ++f) {
+            Q->vis[f] = Q->fv[f][0] >= 0 && qh_dist(Q, f, pe) > eps;
+            if (Q->vis[f]) Q->vl[nvis++] = f;
+        }
+        int nh = 0;
+        for (int j = 0; j < nvis; ++j) {
+            const int* fv = Q->fv[Q->vl[j]];
+            for (int e = 0; e < 3; ++e) {
+                int u = fv[e], w = fv[(e + 1) % 3], twin = 0;
+                for (int m = 0; m < nvis && !twin; ++m) {
+                    const int* gv = Q->fv[Q->vl[m]];
+                    twin = (gv[0] == w && gv[1] == u) || (gv[1] == w && gv[2] == u) || (gv[2] == w && gv[0] == u);
+                }
+                if (!twin) {
+                    if (nh == fcap) return GJKEPA_STATUS_DEGENERATE;   /* cannot fit: see below */
+                    Q->hu[nh] = u; Q->hw[nh] = w; ++nh;
+                }
+            }
+        }
+        if (nh == 0 || hwm + (nh > nvis ? nh - nvis : 0) > fcap) return GJKEPA_STATUS_DEGENERATE;
+        for (int k = 0; k < nh; ++k) Q->ns[k] = k < nvis ? Q->vl[k] : hwm + (k - nvis);
+        /* re-assign the points of removed faces among the new faces (needs the old vis flags) */
+        v3 nnrm[QH_FCAP];
+        for (int k = 0; k < nh; ++k) {
+            nnrm[k] = uninml(Q->p[Q->hu[k]], Q->p[Q->hw[k]], pe);
+            if (is_zero_nml(nnrm[k])) return GJKEPA_STATUS_DEGENERATE;
+        }
+        Q->st[eye] = -1;
+        for (int j = 0; j < n; ++j) {
+            if (Q->st[j] < 0 || !Q->vis[Q->st[j]]) continue;
+            double best = -DBL_MAX; int bk = -1;
+            for (int k = 0; k < nh; ++k) {
+                double d = dot(vsub(Q->p[j], Q->p[Q->hu[k]]), nnrm[k]);
+                if (d > best) { best = d; bk = k; }
+            }
+            if (best > eps) { Q->st[j] = Q->ns[bk]; Q->dist[j] = best; } else Q->st[j] = -1;
+        }
+        for (int j = 0; j < nvis; ++j) Q->vis[Q->vl[j]] = 0;
+        for (int k = nh; k < nvis; ++k) Q->fv[Q->vl[k]][0] = -1;   /* removed slots left over */
+        for (int k = 0; k < nh; ++k) {
+            int s = Q->ns[k];
+            Q->fv[s][0] = Q->hu[k]; Q->fv[s][1] = Q->hw[k]; Q->fv[s][2] = eye;
+            Q->fn[s] = nnrm[k];
+            Q->vis[s] = 0;
+        }
+        if (nh > nvis) hwm += nh - nvis;
+    }
+    /* output: live faces in slot order, then the referenced points in ascending order */
+    int nf = 0;
+    memset(Q->used, 0, sizeof(Q->used));
+    for (int f = 0; f < hwm; ++f) {
+        if (Q->fv[f][0] < 0) continue;
+        for (int e = 0; e < 3; ++e) { faces[3 * nf + e] = Q->fv[f][e]; Q->used[Q->fv[f][e]] = 1; }
+        ++nf;
+    }
+    int nv = 0;
+    for (int j = 0; j < n; ++j) if (Q->used[j]) vidx[nv++] = j;
+    *nf_out = nf; *nv_out = nv;
+    return GJKEPA_STATUS_OK;
+}
+
+int oracle_hull_batch(int32_t vert_dtype, const void* points, const int64_t* cloud_off,
+                      const int32_t* cloud_cnt, int64_t n_clouds, const int64_t* face_off,
+                      int32_t* faces, int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                      void* hull_verts, int32_t* vert_idx, int32_t nthreads) {
+    if (!points || !cloud_off || !cloud_cnt || !face_off || !faces || !n_faces || !n_verts || !status || n_clouds < 0)
+        return GJKEPA_E_ARG;
+    if (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64) return GJKEPA_E_ARG;
+    int nt = nthreads > 0 ? nthreads : oracle_max_threads();
+    (void)nt;
+#pragma omp parallel num_threads(nt)
+    {
+        qhbuf* Q = (qhbuf*)malloc(sizeof(qhbuf));
+        int32_t vi[GJKEPA_HULL_MAX_POINTS];
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t c = 0; c < n_clouds; ++c) {
+            const int n = cloud_cnt[c];
+            int32_t nf = 0, nv = 0;
+            int st = GJKEPA_STATUS_BAD_INPUT;
+            if (n >= 4 && n <= GJKEPA_HULL_MAX_POINTS) {
+                for (int j = 0; j < n; ++j) {
+                    if (vert_dtype == GJKEPA_DTYPE_F64) {
+                        const double* q = (const double*)points + cloud_off[c];
+                        Q->p[j] = mk(q[j], q[n + j], q[2 * n + j]);
+                    } else {
+                        const float* q = (const float*)points + cloud_off[c];
+                        Q->p[j] = mk((double)q[j], (double)q[n + j], (double)q[2 * n + j]);
+                    }
+                }
+                st = qh_cloud(Q, n, faces + 3 * face_off[c], &nf, vi, &nv);
+            }
+            if (st != GJKEPA_STATUS_OK) { nf = 0; nv = 0; }
+            n_faces[c] = nf; n_verts[c] = nv; status[c] = (int8_t)st;
+            for (int k = 0; k < nv; ++k) {
+                if (vert_idx) vert_idx[cloud_off[c] + k] = vi[k];
+                if (!hull_verts) continue;
+                if (vert_dtype == GJKEPA_DTYPE_F64) {
+                    const double* q = (const double*)points + cloud_off[c];
+                    double* h = (double*)hull_verts + cloud_off[c];
+                    h[k] = q[vi[k]]; h[nv + k] = q[n + vi[k]]; h[2 * nv + k] = q[2 * n + vi[k]];
+                } else {
+                    const float* q = (const float*)points + cloud_off[c];
+                    float* h = (float*)hull_verts + cloud_off[c];
+                    h[k] = q[vi[k]]; h[nv + k] = q[n + vi[k]]; h[2 * nv + k] = q[2 * n + vi[k]];
+                }
+            }
+        }
+        free(Q);
+    }
+    return 0;
+}

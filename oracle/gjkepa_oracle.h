@@ -32,6 +32,13 @@ int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
                         const int32_t* pairs, int64_t n_pairs,
                         gjkepa_contact_f64* out, int32_t nthreads);
 
+/* Batched convex hulls (include/gjkepa.h: gjkepa_hull_batch semantics, host buffers, OpenMP over
+ * clouds).  Same arguments as gjkepa_hull_batch minus the size bounds and the device. */
+int oracle_hull_batch(int32_t vert_dtype, const void* points, const int64_t* cloud_off,
+                      const int32_t* cloud_cnt, int64_t n_clouds, const int64_t* face_off,
+                      int32_t* faces, int32_t* n_faces, int32_t* n_verts, int8_t* status,
+                      void* hull_verts, int32_t* vert_idx, int32_t nthreads);
+
 /* Number of OpenMP threads the batch call would use for nthreads <= 0. */
 int oracle_max_threads(void);
 

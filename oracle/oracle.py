@@ -72,3 +72,43 @@ def gjkepa_batch(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0)
 
 def max_threads() -> int:
     return int(load().oracle_max_threads())
+
+
+def hull_face_offsets(cnt) -> np.ndarray:
+    """Triangle offset of each cloud's face block: exclusive prefix sum of 2n - 4 (0 for n < 4)."""
+    cap = np.where(np.asarray(cnt) >= 4, 2 * np.asarray(cnt, np.int64) - 4, 0)
+    off = np.zeros(len(cap), np.int64)
+    if len(cap) > 1:
+        off[1:] = np.cumsum(cap)[:-1]
+    return off
+
+
+def hull_batch(verts, cloud_off, cloud_cnt, nthreads: int = 0) -> dict:
+    """Convex hull of every cloud of a pool (gjkepa_hull_batch semantics).  Returns a dict with
+    faces (int32 [sum(2n-4), 3]), face_off, n_faces, n_verts, status, hull_verts, vert_idx."""
+    verts = np.ascontiguousarray(verts)
+    code = 0 if verts.dtype == np.float32 else 1
+    off = np.ascontiguousarray(cloud_off, np.int64)
+    cnt = np.ascontiguousarray(cloud_cnt, np.int32)
+    n = len(cnt)
+    foff = hull_face_offsets(cnt)
+    nslots = int(foff[-1] + max(2 * int(cnt[-1]) - 4, 0)) if n else 0
+    faces = np.full((max(nslots, 1), 3), -1, np.int32)
+    nf = np.zeros(n, np.int32)
+    nv = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int8)
+    hv = np.zeros_like(verts)
+    vi = np.full(verts.size, -1, np.int32)
+    lib = load()
+    if not hasattr(lib, "_hull_typed"):
+        vp = ctypes.c_void_p
+        lib.oracle_hull_batch.argtypes = [ctypes.c_int32, vp, vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp,
+                                          ctypes.c_int32]
+        lib.oracle_hull_batch.restype = ctypes.c_int
+        lib._hull_typed = True
+    rc = lib.oracle_hull_batch(code, verts.ctypes.data, off.ctypes.data, cnt.ctypes.data, n, foff.ctypes.data,
+                               faces.ctypes.data, nf.ctypes.data, nv.ctypes.data, st.ctypes.data, hv.ctypes.data,
+                               vi.ctypes.data, int(nthreads))
+    assert rc == 0
+    return dict(faces=faces[:nslots], face_off=foff, n_faces=nf, n_verts=nv, status=st, hull_verts=hv,
+                vert_idx=vi)
