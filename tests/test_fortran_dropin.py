@@ -35,3 +35,46 @@ def test_fortran_gjkepa_matches_oracle(orc):
         assert np.all((vals == want) | both_nan), (f, want)
     mism = [ln for ln in out.stdout.splitlines() if ln.startswith("OMP_MISMATCH")]
     assert mism and int(mism[0].split()[1]) == 0, "OpenMP callers disagree with the batched entry"
+
+
+QH_EXE = os.path.join(ROOT, "tests", "fortran", "build", "test_quickhull")
+
+
+def test_quickhull_driver_built():
+    assert os.path.exists(QH_EXE), "run __graft_entry__.build()"
+
+
+@pytest.mark.gpu
+def test_fortran_quickhull_matches_oracle(orc, tmp_path):
+    """USE GCLIB_QuickHull / GCLIB_DeHull; CALL QuickHull(points, polytope, info) and
+    getHullMeshesVertex(polytope, points, info) with the reference's call-site argument lists
+    (GCLIB_GJKEPA.f90:920, :950), plus QUICKHULL_BATCH, against the oracle hull."""
+    import gjkepa
+    rng = np.random.default_rng(8)
+    clouds = [np.r_[CUBE, [[0.5, 0.5, 0.5]]], rng.normal(size=(40, 3)), rng.uniform(-1, 1, (200, 3)),
+              np.c_[rng.normal(size=(12, 2)), np.zeros(12)], rng.normal(size=(3, 3))]
+    clouds = [np.asarray(c, np.float32).astype(np.float64) for c in clouds]
+    path = tmp_path / "clouds.txt"
+    with open(path, "w") as fh:
+        fh.write(f"{len(clouds)}\n")
+        for c in clouds:
+            fh.write(f"{len(c)}\n" + "".join(f"{x:.17g} {y:.17g} {z:.17g}\n" for x, y, z in c))
+    out = subprocess.run([QH_EXE, str(path)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    pool = gjkepa.CloudPool.from_list(clouds)
+    r = orc.hull_batch(pool.verts, pool.cloud_off, pool.cloud_cnt)
+    lines = out.stdout.splitlines()
+    q = [i for i, ln in enumerate(lines) if ln.startswith("Q ")]
+    b = [ln.split() for ln in lines if ln.startswith("B ")]
+    assert len(q) == len(clouds) == len(b)
+    for c, i in enumerate(q):
+        _, _, info, nf, nv = lines[i].split()
+        assert int(info) == r["status"][c] and int(nf) == r["n_faces"][c] and int(nv) == r["n_verts"][c]
+        fo = r["face_off"][c]
+        want = clouds[c][r["faces"][fo:fo + r["n_faces"][c]]].reshape(-1, 9)
+        got = np.array([[float(x) for x in lines[i + 1 + f].split()[1:]] for f in range(int(nf))]).reshape(-1, 9)
+        np.testing.assert_array_equal(got, want)
+        st, nfb, nvb = int(b[c][2]), int(b[c][3]), int(b[c][4])
+        assert (st, nfb, nvb) == (r["status"][c], r["n_faces"][c], r["n_verts"][c])
+        tri = np.array([int(x) for x in b[c][5:]]).reshape(-1, 3) - 1
+        np.testing.assert_array_equal(tri, r["faces"][fo:fo + nfb])
