@@ -17,6 +17,7 @@
 #include "../../include/gjkepa.h"
 #include "gjkepa_kernel.h"
 #include "hull_kernel.h"
+#include "broadphase_kernel.h"
 
 namespace {
 
@@ -55,6 +56,7 @@ struct DeviceState {
     hipStream_t stream = nullptr;
     DevBuf verts, off, cnt, pairs, out, ws;
     DevBuf h_foff, h_faces, h_nf, h_nv, h_st, h_hv, h_vi;   // gjkepa_hull_batch staging
+    DevBuf b_pairs, b_count, b_ws;                          // gjkepa_broadphase staging
 };
 
 std::mutex g_table_mu;
@@ -373,6 +375,81 @@ int gjkepa_hull_batch(int32_t vert_dtype, const void* points, int64_t n_point_sc
                         (size_t)(3 * nv) * esz);
         if (nv && vert_idx) std::memcpy(vert_idx + cloud_off[c], hi.data() + cloud_off[c], (size_t)nv * 4);
     }
+    return 0;
+}
+
+// ---- device broad phase (include/gjkepa.h) --------------------------------
+int64_t gjkepa_broadphase_workspace_bytes(int64_t n_hulls, int64_t max_pairs) {
+    if (n_hulls < 0 || max_pairs < 0 || n_hulls > INT32_MAX - 1 || max_pairs > INT32_MAX) return GJKEPA_E_ARG;
+    const int64_t b = gjkepa_broadphase_ws_bytes(n_hulls, max_pairs);
+    return b < 0 ? fail(GJKEPA_E_NODEVICE, "workspace query needs a HIP device") : b;
+}
+
+int gjkepa_broadphase_device(int32_t vert_dtype, const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                             int64_t n_hulls, int32_t* pairs, int64_t max_pairs, int64_t* n_pairs, void* workspace,
+                             int64_t workspace_bytes, void* stream) {
+    if (n_hulls < 0 || max_pairs < 0 || n_hulls > INT32_MAX - 1 || max_pairs > INT32_MAX ||
+        (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64))
+        return fail(GJKEPA_E_ARG, "bad n_hulls/max_pairs/dtype");
+    if (!n_pairs) return fail(GJKEPA_E_ARG, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    if (n_hulls == 0) {
+        e = hipMemsetAsync(n_pairs, 0, 8, s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    if (!verts || !hull_off || !hull_cnt || !workspace || (max_pairs > 0 && !pairs)) return fail(GJKEPA_E_ARG, "null pointer");
+    bool small = false;
+    e = gjkepa_enqueue_broadphase(vert_dtype, verts, hull_off, hull_cnt, n_hulls, pairs, max_pairs, n_pairs, workspace,
+                                  workspace_bytes, s, &small);
+    if (e != hipSuccess) return hip_fail(e, "broad phase launch");
+    return small ? fail(GJKEPA_E_WORKSPACE, "workspace too small") : 0;
+}
+
+int gjkepa_broadphase(int32_t vert_dtype, const void* verts, int64_t n_vert_scalars, const int64_t* hull_off,
+                      const int32_t* hull_cnt, int64_t n_hulls, int32_t* pairs, int64_t max_pairs, int64_t* n_pairs,
+                      int32_t device) {
+    if (n_hulls < 0 || max_pairs < 0 || n_vert_scalars < 0 || n_hulls > INT32_MAX - 1 || max_pairs > INT32_MAX ||
+        (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64))
+        return fail(GJKEPA_E_ARG, "bad sizes/dtype");
+    if (!n_pairs || (max_pairs > 0 && !pairs)) return fail(GJKEPA_E_ARG, "null pointer");
+    *n_pairs = 0;
+    if (n_hulls == 0) return 0;
+    if (!verts || !hull_off || !hull_cnt) return fail(GJKEPA_E_ARG, "null pointer");
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        const int64_t c = hull_cnt[h];
+        if (c >= 1 && c <= GJKEPA_MAX_HULL_VERTS && (hull_off[h] < 0 || hull_off[h] + 3 * c > n_vert_scalars))
+            return fail(GJKEPA_E_ARG, "hull outside the vertex pool");
+    }
+    int rc = 0;
+    DeviceState* d = device_state(device, &rc);
+    if (!d) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    if ((rc = init_device(d, device))) return rc;
+    const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
+    const int64_t wsb = gjkepa_broadphase_ws_bytes(n_hulls, max_pairs);
+    if (wsb < 0) return fail(GJKEPA_E_HIP, "broad phase workspace query failed");
+    hipError_t e;
+    if ((e = d->verts.ensure((size_t)n_vert_scalars * esz)) != hipSuccess || (e = d->off.ensure((size_t)n_hulls * 8)) != hipSuccess ||
+        (e = d->cnt.ensure((size_t)n_hulls * 4)) != hipSuccess || (e = d->b_pairs.ensure((size_t)max_pairs * 8 + 8)) != hipSuccess ||
+        (e = d->b_count.ensure(8)) != hipSuccess || (e = d->b_ws.ensure((size_t)wsb)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    hipStream_t s = d->stream;
+    if ((e = hipMemcpyAsync(d->verts.p, verts, (size_t)n_vert_scalars * esz, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->off.p, hull_off, (size_t)n_hulls * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->cnt.p, hull_cnt, (size_t)n_hulls * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    rc = gjkepa_broadphase_device(vert_dtype, d->verts.p, (const int64_t*)d->off.p, (const int32_t*)d->cnt.p, n_hulls,
+                                  (int32_t*)d->b_pairs.p, max_pairs, (int64_t*)d->b_count.p, d->b_ws.p,
+                                  (int64_t)d->b_ws.cap, s);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(n_pairs, d->b_count.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    const int64_t m = *n_pairs < max_pairs ? *n_pairs : max_pairs;
+    if (m > 0 && ((e = hipMemcpyAsync(pairs, d->b_pairs.p, (size_t)m * 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                  (e = hipStreamSynchronize(s)) != hipSuccess))
+        return hip_fail(e, "hipMemcpyAsync D2H");
     return 0;
 }
 

@@ -140,3 +140,43 @@ extern "C" int64_t gjkepa_synth_clouds(uint64_t seed, int64_t first_cloud, int64
     }
     return total;
 }
+
+// Scene for the broad phase: hull h has n ~ U{n_min..n_max} unit-sphere
+// vertices about a centre uniform in [0, box)^3.  Streams keyed by the global hull index.
+extern "C" int64_t gjkepa_synth_scene(uint64_t seed, int64_t first_hull, int64_t n_hulls,
+                                      int32_t n_min, int32_t n_max, double box,
+                                      int32_t vert_dtype, void* verts, int64_t* hull_off, int32_t* hull_cnt) {
+    if (n_hulls < 0 || n_min < 1 || n_max < n_min || n_max > GJKEPA_MAX_HULL_VERTS || !(box >= 0.0)) return GJKEPA_E_ARG;
+    if (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64) return GJKEPA_E_ARG;
+    std::vector<int32_t> cnt((size_t)n_hulls);
+#pragma omp parallel for schedule(static)
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        PairRng g(seed ^ 0x5CE7Eull, first_hull + h);
+        cnt[h] = draw_n(g, n_min, n_max);
+    }
+    std::vector<int64_t> off((size_t)n_hulls + 1);
+    off[0] = 0;
+    for (int64_t h = 0; h < n_hulls; ++h) off[h + 1] = off[h] + 3 * (int64_t)cnt[h];
+    const int64_t total = off[n_hulls];
+    if (!verts) return total;
+    if (!hull_off || !hull_cnt) return GJKEPA_E_ARG;
+#pragma omp parallel for schedule(static)
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        PairRng g(seed ^ 0x5CE7Eull, first_hull + h);
+        const int32_t n = draw_n(g, n_min, n_max);
+        const double c[3] = {box * g.u01(), box * g.u01(), box * g.u01()};
+        const int64_t o = off[h];
+        for (int32_t i = 0; i < n; ++i) {
+            double v[3];
+            unit_vec(g, v);
+            for (int d = 0; d < 3; ++d) {
+                const float val = (float)(v[d] + c[d]);
+                if (vert_dtype == GJKEPA_DTYPE_F32) ((float*)verts)[o + (int64_t)d * n + i] = val;
+                else ((double*)verts)[o + (int64_t)d * n + i] = (double)val;
+            }
+        }
+        hull_off[h] = o;
+        hull_cnt[h] = n;
+    }
+    return total;
+}

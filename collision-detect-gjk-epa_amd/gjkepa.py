@@ -31,6 +31,7 @@ EXPORTS = (
     "gjkepa_record_bytes", "gjkepa_query", "gjkepa_batch", "gjkepa_workspace_bytes",
     "gjkepa_batch_device", "gjkepa_last_error", "gjkepa_version_string", "gjkepa_synth_pairs",
     "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
+    "gjkepa_broadphase_workspace_bytes", "gjkepa_broadphase", "gjkepa_broadphase_device", "gjkepa_synth_scene",
 )
 HULL_MAX_POINTS = 256
 
@@ -99,6 +100,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_hull_batch_device.restype = ctypes.c_int
     lib.gjkepa_synth_clouds.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]
     lib.gjkepa_synth_clouds.restype = c_i64
+    lib.gjkepa_broadphase_workspace_bytes.argtypes = [c_i64, c_i64]
+    lib.gjkepa_broadphase_workspace_bytes.restype = c_i64
+    lib.gjkepa_broadphase.argtypes = [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32]
+    lib.gjkepa_broadphase.restype = ctypes.c_int
+    lib.gjkepa_broadphase_device.argtypes = [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]
+    lib.gjkepa_broadphase_device.restype = ctypes.c_int
+    lib.gjkepa_synth_scene.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp]
+    lib.gjkepa_synth_scene.restype = c_i64
     if path is None:
         _lib = lib
     return lib
@@ -343,3 +352,52 @@ def hull_mesh_vertices(polytope) -> np.ndarray:
     v = np.asarray(polytope, np.float64).reshape(-1, 3)
     _, first = np.unique(v, axis=0, return_index=True)
     return v[np.sort(first)]
+
+
+# ---- device broad phase (include/gjkepa.h gjkepa_broadphase) -----------------
+def synth_scene(seed: int, n_hulls: int, n_min: int = 32, n_max: int = 32, box: float = 10.0,
+                first_hull: int = 0, dtype=np.float32) -> HullPool:
+    """Deterministic scene: unit-sphere hulls centred uniformly in [0, box)^3 (pairs left empty)."""
+    lib = load()
+    code = DTYPE_F32 if np.dtype(dtype) == np.float32 else DTYPE_F64
+    total = lib.gjkepa_synth_scene(seed, first_hull, n_hulls, n_min, n_max, box, code, None, None, None)
+    if total < 0:
+        raise GjkEpaError("gjkepa_synth_scene: bad arguments")
+    verts = np.empty(total, dtype=dtype)
+    off = np.empty(n_hulls, np.int64)
+    cnt = np.empty(n_hulls, np.int32)
+    lib.gjkepa_synth_scene(seed, first_hull, n_hulls, n_min, n_max, box, code, _ptr(verts), _ptr(off), _ptr(cnt))
+    return HullPool(verts, off, cnt, np.zeros((0, 2), np.int32))
+
+
+def broadphase(pool: HullPool, max_pairs: int | None = None, device: int = 0):
+    """Candidate pairs (a < b, ascending) passing the reference's sphere test, on the GPU.
+    Returns (pairs int32 [n, 2], n_found); with max_pairs None the list is grown until it fits."""
+    lib = load()
+    verts = np.ascontiguousarray(pool.verts)
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    cap = max_pairs if max_pairs is not None else max(16 * cnt.size, 1024)
+    while True:
+        out = np.zeros((max(cap, 1), 2), np.int32)
+        nf = np.zeros(1, np.int64)
+        rc = lib.gjkepa_broadphase(pool.dtype_code, _ptr(verts), verts.size, _ptr(off), _ptr(cnt), cnt.size, _ptr(out),
+                                   cap, _ptr(nf), int(device))
+        _check(rc, "gjkepa_broadphase")
+        n = int(nf[0])
+        if n <= cap or max_pairs is not None:
+            return out[:min(n, cap)], n
+        cap = n
+
+
+def broadphase_workspace_bytes(n_hulls: int, max_pairs: int) -> int:
+    return int(load().gjkepa_broadphase_workspace_bytes(n_hulls, max_pairs))
+
+
+def broadphase_device(vert_dtype: int, verts_ptr: int, hull_off_ptr: int, hull_cnt_ptr: int, n_hulls: int,
+                      pairs_ptr: int, max_pairs: int, n_pairs_ptr: int, ws_ptr: int, ws_bytes: int,
+                      stream: int = 0) -> None:
+    """Device-resident broad phase (raw device pointers), asynchronous on `stream`."""
+    rc = load().gjkepa_broadphase_device(int(vert_dtype), verts_ptr, hull_off_ptr, hull_cnt_ptr, int(n_hulls),
+                                         pairs_ptr, int(max_pairs), n_pairs_ptr, ws_ptr, int(ws_bytes), stream or None)
+    _check(rc, "gjkepa_broadphase_device")

@@ -192,6 +192,37 @@ int gjkepa_hull_batch_device(int32_t vert_dtype, const void* points,
                              int32_t* n_faces, int32_t* n_verts, int8_t* status,
                              void* hull_verts, int32_t* vert_idx, void* stream);
 
+/* ---- device broad phase -------------------------------------------------
+ * Emits the candidate pair list a narrow-phase batch consumes: every pair of hulls (a < b) of a
+ * pool whose bounding spheres pass the reference's own rough test,
+ * RoughCollisionDetection_SphericalEnvelope (GCLIB_GJKEPA.f90:1165-1188):
+ *   m = SUM(p(:,k)) / n (sequential sums), r = MAXVAL(NORM2(p_i - m)),
+ *   pair iff NORM2(m_a - m_b) <= r_a + r_b + 1.0      (fp64, the oracle's arithmetic, bit-exact)
+ * i.e. exactly the pairs whose GJKEPA call would get past its first test (:76-80); a caller's
+ * double loop over all pairs collapses to this list.  Hulls with a bad vertex count or non-finite
+ * coordinates take part in no pair.
+ *
+ * Method (MI355X): per-hull sphere kernel; radix sort of the spheres' x-extent lower bounds
+ * (rocPRIM); sweep kernels (count, exclusive scan, emit) test each sphere against the ones after
+ * it in x order until the extents separate; a final radix sort of the emitted (a << 32 | b) keys
+ * leaves the list in ascending (a, b) order — the order of `DO a = 1, N; DO b = a+1, N`.
+ * Output: pairs[2k], pairs[2k+1] = (a, b) for k < min(n_found, max_pairs); *n_pairs = n_found
+ * (device int64 for the device entry).  n_found > max_pairs means the list was cut: enlarge it and
+ * call again.  The device entry never synchronises (graph-capturable): the final sort runs over
+ * max_pairs keys padded with all-ones, so size max_pairs near the expected count. */
+int64_t gjkepa_broadphase_workspace_bytes(int64_t n_hulls, int64_t max_pairs);
+
+/* Host buffers, blocking.  *n_pairs = pairs found (the list holds the first max_pairs of them). */
+int gjkepa_broadphase(int32_t vert_dtype, const void* verts, int64_t n_vert_scalars,
+                      const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
+                      int32_t* pairs, int64_t max_pairs, int64_t* n_pairs, int32_t device);
+
+/* Device buffers, asynchronous on `stream`; n_pairs is a device int64. */
+int gjkepa_broadphase_device(int32_t vert_dtype, const void* verts, const int64_t* hull_off,
+                             const int32_t* hull_cnt, int64_t n_hulls,
+                             int32_t* pairs, int64_t max_pairs, int64_t* n_pairs,
+                             void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Last error message of the calling thread ("" if none). */
 const char* gjkepa_last_error(void);
 
@@ -219,6 +250,13 @@ int64_t gjkepa_synth_clouds(uint64_t seed, int64_t first_cloud, int64_t n_clouds
                             int32_t n_min, int32_t n_max, int32_t shape,
                             int32_t vert_dtype, void* verts,
                             int64_t* cloud_off, int32_t* cloud_cnt);
+
+/* Synthetic scene for the broad phase: n_hulls hulls of n ~ U{n_min..n_max} unit-sphere vertices
+ * (as gjkepa_synth_pairs' hull A) centred uniformly in the cube [0, box)^3; counter-based per
+ * global hull index, fp32-rounded; verts == NULL returns the scalar count. */
+int64_t gjkepa_synth_scene(uint64_t seed, int64_t first_hull, int64_t n_hulls,
+                           int32_t n_min, int32_t n_max, double box,
+                           int32_t vert_dtype, void* verts, int64_t* hull_off, int32_t* hull_cnt);
 
 #ifdef __cplusplus
 }

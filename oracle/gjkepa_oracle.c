@@ -957,3 +957,112 @@ int oracle_hull_batch(int32_t vert_dtype, const void* points, const int64_t* clo
     }
     return 0;
 }
+
+/* ==== broad phase ==========================================================
+ * Every pair (a < b) of a hull pool passing RoughCollisionDetection_SphericalEnvelope (:1165-1188),
+ * in ascending (a, b) order.  Centres / radii use sphere_test's arithmetic (hull_mean, max norm2);
+ * candidates come from a uniform grid of cell size >= 2 r_max + 1 (27 neighbour cells), so the
+ * search is complete, and every candidate is decided by the exact predicate. */
+typedef struct { int64_t key; int32_t h; } bp_cell;
+static int bp_cmp_cell(const void* x, const void* y) {
+    const bp_cell *a = (const bp_cell*)x, *b = (const bp_cell*)y;
+    return a->key < b->key ? -1 : a->key > b->key ? 1 : (a->h < b->h ? -1 : a->h > b->h);
+}
+static int bp_cmp_u64(const void* x, const void* y) {
+    uint64_t a = *(const uint64_t*)x, b = *(const uint64_t*)y;
+    return a < b ? -1 : a > b;
+}
+
+int oracle_broadphase(int32_t vert_dtype, const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                      int64_t n_hulls, int32_t* pairs, int64_t max_pairs, int64_t* n_pairs, int32_t nthreads) {
+    if (!verts || !hull_off || !hull_cnt || !n_pairs || n_hulls < 0 || max_pairs < 0 || (max_pairs > 0 && !pairs))
+        return GJKEPA_E_ARG;
+    if (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64) return GJKEPA_E_ARG;
+    int nt = nthreads > 0 ? nthreads : oracle_max_threads();
+    (void)nt;
+    v3* m = (v3*)malloc(sizeof(v3) * (size_t)(n_hulls + 1));
+    double* r = (double*)malloc(sizeof(double) * (size_t)(n_hulls + 1));
+    unsigned char* ok = (unsigned char*)malloc((size_t)n_hulls + 1);
+#pragma omp parallel num_threads(nt)
+    {
+        double* buf = (double*)malloc(sizeof(double) * 3 * GJKEPA_MAX_HULL_VERTS);
+#pragma omp for schedule(static)
+        for (int64_t h = 0; h < n_hulls; ++h) {
+            const int n = hull_cnt[h];
+            ok[h] = 0;
+            if (n < 1 || n > GJKEPA_MAX_HULL_VERTS) continue;
+            hull_t A;
+            if (vert_dtype == GJKEPA_DTYPE_F64) {
+                A.p = (const double*)verts + hull_off[h];
+            } else {
+                const float* f = (const float*)verts + hull_off[h];
+                for (int i = 0; i < 3 * n; ++i) buf[i] = (double)f[i];
+                A.p = buf;
+            }
+            A.n = n;
+            m[h] = hull_mean(&A);
+            double rr = -DBL_MAX;
+            for (int i = 0; i < n; ++i) { double t = norm2(vsub(hv(&A, i), m[h])); if (t > rr) rr = t; }
+            r[h] = rr;
+            ok[h] = isfinite(m[h].x) && isfinite(m[h].y) && isfinite(m[h].z) && isfinite(rr);
+        }
+        free(buf);
+    }
+    double rmax = 0.0;
+    for (int64_t h = 0; h < n_hulls; ++h) if (ok[h] && r[h] > rmax) rmax = r[h];
+    const double cell = (2.0 * rmax + SPHERE_TOL) * (1.0 + 1e-9) + 1e-9;
+    bp_cell* cells = (bp_cell*)malloc(sizeof(bp_cell) * (size_t)(n_hulls + 1));
+    int64_t nc = 0;
+    const int64_t B = 1 << 20;                  /* cell coordinates packed 21 bits each */
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        if (!ok[h]) continue;
+        int64_t ix = (int64_t)floor(m[h].x / cell) + B, iy = (int64_t)floor(m[h].y / cell) + B,
+                iz = (int64_t)floor(m[h].z / cell) + B;
+        cells[nc].key = (ix << 42) | (iy << 21) | iz;
+        cells[nc].h = (int32_t)h;
+        ++nc;
+    }
+    qsort(cells, (size_t)nc, sizeof(bp_cell), bp_cmp_cell);
+    uint64_t* found = NULL;
+    int64_t nfound = 0, cap = 0;
+#pragma omp parallel num_threads(nt)
+    {
+        uint64_t* loc = NULL;
+        int64_t nl = 0, cl = 0;
+#pragma omp for schedule(dynamic, 256)
+        for (int64_t s = 0; s < nc; ++s) {
+            const int64_t key = cells[s].key;
+            const int32_t a = cells[s].h;
+            const int64_t ix = key >> 42, iy = (key >> 21) & ((1 << 21) - 1), iz = key & ((1 << 21) - 1);
+            for (int dx = -1; dx <= 1; ++dx)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dz = -1; dz <= 1; ++dz) {
+                        const int64_t k2 = ((ix + dx) << 42) | ((iy + dy) << 21) | (iz + dz);
+                        int64_t lo = 0, hi = nc;                  /* first cell entry with key >= k2 */
+                        while (lo < hi) { int64_t md = (lo + hi) / 2; if (cells[md].key < k2) lo = md + 1; else hi = md; }
+                        for (int64_t t = lo; t < nc && cells[t].key == k2; ++t) {
+                            const int32_t b = cells[t].h;
+                            if (b <= a) continue;
+                            if (!(norm2(vsub(m[a], m[b])) <= r[a] + r[b] + SPHERE_TOL)) continue;
+                            if (nl == cl) { cl = cl ? 2 * cl : 1024; loc = (uint64_t*)realloc(loc, sizeof(uint64_t) * (size_t)cl); }
+                            loc[nl++] = ((uint64_t)a << 32) | (uint32_t)b;
+                        }
+                    }
+        }
+#pragma omp critical
+        {
+            if (nfound + nl > cap) { cap = 2 * (nfound + nl) + 1024; found = (uint64_t*)realloc(found, sizeof(uint64_t) * (size_t)cap); }
+            if (nl) memcpy(found + nfound, loc, sizeof(uint64_t) * (size_t)nl);
+            nfound += nl;
+        }
+        free(loc);
+    }
+    qsort(found, (size_t)nfound, sizeof(uint64_t), bp_cmp_u64);
+    for (int64_t k = 0; k < nfound && k < max_pairs; ++k) {
+        pairs[2 * k] = (int32_t)(found[k] >> 32);
+        pairs[2 * k + 1] = (int32_t)(found[k] & 0xffffffffu);
+    }
+    *n_pairs = nfound;
+    free(found); free(cells); free(m); free(r); free(ok);
+    return 0;
+}

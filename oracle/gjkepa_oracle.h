@@ -39,6 +39,11 @@ int oracle_hull_batch(int32_t vert_dtype, const void* points, const int64_t* clo
                       int32_t* faces, int32_t* n_faces, int32_t* n_verts, int8_t* status,
                       void* hull_verts, int32_t* vert_idx, int32_t nthreads);
 
+/* Broad phase (include/gjkepa.h: gjkepa_broadphase semantics): every pair a < b passing the
+ * reference's sphere test, ascending (a, b); *n_pairs = number found, first max_pairs written. */
+int oracle_broadphase(int32_t vert_dtype, const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                      int64_t n_hulls, int32_t* pairs, int64_t max_pairs, int64_t* n_pairs, int32_t nthreads);
+
 /* Number of OpenMP threads the batch call would use for nthreads <= 0. */
 int oracle_max_threads(void);
 

@@ -112,3 +112,28 @@ def hull_batch(verts, cloud_off, cloud_cnt, nthreads: int = 0) -> dict:
     assert rc == 0
     return dict(faces=faces[:nslots], face_off=foff, n_faces=nf, n_verts=nv, status=st, hull_verts=hv,
                 vert_idx=vi)
+
+
+def broadphase(verts, hull_off, hull_cnt, max_pairs: int = -1, nthreads: int = 0):
+    """Every pair a < b passing the reference's sphere test, ascending (a, b).  Returns
+    (pairs int32 [n, 2], n_found)."""
+    verts = np.ascontiguousarray(verts)
+    code = 0 if verts.dtype == np.float32 else 1
+    off = np.ascontiguousarray(hull_off, np.int64)
+    cnt = np.ascontiguousarray(hull_cnt, np.int32)
+    lib = load()
+    if not hasattr(lib, "_bp_typed"):
+        vp = ctypes.c_void_p
+        lib.oracle_broadphase.argtypes = [ctypes.c_int32, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, vp,
+                                          ctypes.c_int32]
+        lib.oracle_broadphase.restype = ctypes.c_int
+        lib._bp_typed = True
+    nf = np.zeros(1, np.int64)
+    if max_pairs < 0:   # size query first
+        assert lib.oracle_broadphase(code, verts.ctypes.data, off.ctypes.data, cnt.ctypes.data, cnt.size, None, 0,
+                                     nf.ctypes.data, int(nthreads)) == 0
+        max_pairs = int(nf[0])
+    out = np.zeros((max(max_pairs, 1), 2), np.int32)
+    assert lib.oracle_broadphase(code, verts.ctypes.data, off.ctypes.data, cnt.ctypes.data, cnt.size, out.ctypes.data,
+                                 max_pairs, nf.ctypes.data, int(nthreads)) == 0
+    return out[:min(max_pairs, int(nf[0]))], int(nf[0])
