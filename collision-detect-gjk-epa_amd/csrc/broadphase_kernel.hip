@@ -7,16 +7,17 @@
 // (hull_mean, sphere_test), so the list is identical to the oracle's, in ascending (a, b) order.
 //
 // Pipeline on one stream, no host synchronisation (graph-capturable):
-//   1. sphere_kernel   one thread per hull: centre, radius, x-extent [lo, hi] widened by 0.5 + a
-//                      relative margin (the sweep only has to be conservative; the exact test
-//                      decides); invalid hulls get lo = +inf so they sort last and match nothing.
-//   2. radix sort of (lo, hull) pairs (rocPRIM via hipCUB), then gather of the spheres into
-//      x order so the sweep reads consecutive entries.
-//   3. sweep_kernel<count>  thread p tests the spheres after it in x order while lo_q <= hi_p;
-//      exclusive scan of the counts; sweep_kernel<emit> writes (a << 32 | b) keys at the offsets.
-//   4. radix sort of the max_pairs keys (padded with all-ones), unpack to int32 (a, b) pairs.
-// The sweep is HBM/L2-streaming integer-and-fp64 work, no MFMA: each thread walks a contiguous
-// run of the sorted arrays, so neighbouring threads share cache lines.
+//   1. sphere_kernel  16 lanes per hull (LDS-staged coalesced loads): centre, radius, validity;
+//                     the largest radius (atomicMax on the bit pattern, one atomic per block).
+//   2. key_kernel     uniform grid of edge 2 r_max + 1 (every passing pair lies in neighbouring
+//                     cells); 63-bit cell keys (iz, iy, ix), coordinates wrapped at 2^21.
+//   3. radix sort of (cell key, hull) pairs (rocPRIM via hipCUB); gather of the spheres into cell
+//      order, so neighbouring threads read neighbouring entries.
+//   4. grid_kernel<count>: thread p binary-searches the 9 cell rows (ix-1..ix+1 is one key range)
+//      around its cell and tests the hulls there with a larger index; exclusive scan of the counts;
+//      grid_kernel<emit> writes (a << 32 | b) keys at the offsets.
+//   5. radix sort of the max_pairs keys (padded with all-ones); unpack to int32 (a, b) pairs.
+// Memory-latency-bound integer / fp64 work (binary searches, short candidate runs), no MFMA.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -27,82 +28,177 @@
 #include "../../include/gjkepa.h"
 #include "broadphase_kernel.h"
 
+#define DEV_BP __device__ __forceinline__
+
 namespace gk {
 namespace bp {
 
-constexpr double kTol = 1.0;   // TOL of RoughCollisionDetection_SphericalEnvelope (:1172)
+constexpr double kTol = 1.0;               // TOL of RoughCollisionDetection_SphericalEnvelope (:1172)
+constexpr uint64_t kMask = (1ull << 21) - 1;
+constexpr uint64_t kInvalid = ~0ull;
 
+DEV_BP uint64_t cell_key(uint64_t ix, uint64_t iy, uint64_t iz) { return ((iz & kMask) << 42) | ((iy & kMask) << 21) | (ix & kMask); }
+
+// centre, radius and validity of every hull; the largest radius via one atomic per block.
+// A group of SG lanes owns a hull: the group stages the hull's 3n scalars in LDS with coalesced
+// loads, three lanes form the x / y / z sums sequentially in index order (the reference's SUM, so
+// the centre is bit-exact), then every lane takes vertices gl, gl+SG, ... for the radius (a max,
+// order-free).  One thread per hull instead would issue 64 scattered loads per instruction.
+constexpr int SG = 16;
+constexpr int SPHERE_BLOCK = 128;   // 8 hulls per block: 24 KB (fp32) / 48 KB (fp64) of LDS staging
 template <typename TIn>
-__global__ __launch_bounds__(256) void sphere_kernel(const TIn* __restrict__ verts, const int64_t* __restrict__ hull_off,
-                                                     const int32_t* __restrict__ hull_cnt, int64_t n_hulls,
-                                                     double* __restrict__ cx, double* __restrict__ cy,
-                                                     double* __restrict__ cz, double* __restrict__ cr,
-                                                     double* __restrict__ lo, double* __restrict__ hi,
-                                                     int32_t* __restrict__ idx) {
-    for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < n_hulls; h += (int64_t)gridDim.x * blockDim.x) {
-        const int n = hull_cnt[h];
-        double mx = NAN, my = NAN, mz = NAN, r = NAN;
-        if (n >= 1 && n <= GJKEPA_MAX_HULL_VERTS) {
+__global__ __launch_bounds__(SPHERE_BLOCK) void sphere_kernel(const TIn* __restrict__ verts, const int64_t* __restrict__ hull_off,
+                                                              const int32_t* __restrict__ hull_cnt, int64_t n_hulls,
+                                                              double* __restrict__ cx, double* __restrict__ cy,
+                                                              double* __restrict__ cz, double* __restrict__ cr,
+                                                              unsigned long long* __restrict__ rmax_bits) {
+    constexpr int GPB = SPHERE_BLOCK / SG;
+    __shared__ TIn stage[GPB][3 * GJKEPA_MAX_HULL_VERTS];
+    __shared__ double cen[GPB][3];
+    __shared__ unsigned long long blk;
+    const int gl = threadIdx.x % SG, grp = threadIdx.x / SG;
+    if (threadIdx.x == 0) blk = 0;
+    __syncthreads();
+    unsigned long long mine = 0;
+    for (int64_t base = blockIdx.x * (int64_t)GPB; base < n_hulls; base += (int64_t)gridDim.x * GPB) {
+        const int64_t h = base + grp;
+        const int n = h < n_hulls ? hull_cnt[h] : 0;
+        const bool in = h < n_hulls && n >= 1 && n <= GJKEPA_MAX_HULL_VERTS;
+        if (in) {
             const TIn* p = verts + hull_off[h];
-            // SUM(p(:,k)) / SIZE(p,1), sequential in index order (:1175-1176)
-            double sx = 0.0, sy = 0.0, sz = 0.0;
-            for (int i = 0; i < n; ++i) { sx += (double)p[i]; sy += (double)p[n + i]; sz += (double)p[2 * n + i]; }
-            const double dn = (double)n;
-            mx = sx / dn; my = sy / dn; mz = sz / dn;
-            // MAXVAL(NORM2(p(i,:) - mp)) (:1179-1182)
-            r = -DBL_MAX;
-            for (int i = 0; i < n; ++i) {
-                const double dx = (double)p[i] - mx, dy = (double)p[n + i] - my, dz = (double)p[2 * n + i] - mz;
+            for (int i = gl; i < 3 * n; i += SG) stage[grp][i] = p[i];
+        }
+        __syncthreads();
+        const TIn* q = stage[grp];
+        if (in && gl < 3) {   // SUM(p(:,k)) / SIZE(p,1), sequential in index order (:1175-1176)
+            double sum = 0.0;
+            for (int i = 0; i < n; ++i) sum += (double)q[gl * n + i];
+            cen[grp][gl] = sum / (double)n;
+        }
+        __syncthreads();
+        double r = -DBL_MAX;
+        const double mx = cen[grp][0], my = cen[grp][1], mz = cen[grp][2];
+        if (in) {             // MAXVAL(NORM2(p(i,:) - mp)) (:1179-1182)
+            for (int i = gl; i < n; i += SG) {
+                const double dx = (double)q[i] - mx, dy = (double)q[n + i] - my, dz = (double)q[2 * n + i] - mz;
                 const double t = ::sqrt(dx * dx + dy * dy + dz * dz);
                 r = t > r ? t : r;
             }
         }
-        cx[h] = mx; cy[h] = my; cz[h] = mz; cr[h] = r;
-        const bool ok = isfinite(mx) && isfinite(my) && isfinite(mz) && isfinite(r);
-        // conservative x extent: rounding of the exact test is ~1e-16 relative, the margin 1e-9
-        const double half = 0.5 * kTol + r, e = 1e-9 * (1.0 + fabs(mx) + r);
-        lo[h] = ok ? (mx - half) - e : INFINITY;
-        hi[h] = ok ? (mx + half) + e : -INFINITY;
+#pragma unroll
+        for (int m = SG / 2; m >= 1; m /= 2) {
+            const double o = __shfl_xor(r, m, SG);
+            r = o > r ? o : r;
+        }
+        if (h < n_hulls && gl == 0) {
+            const bool ok = in && isfinite(mx) && isfinite(my) && isfinite(mz) && isfinite(r);
+            cx[h] = in ? mx : NAN; cy[h] = in ? my : NAN; cz[h] = in ? mz : NAN; cr[h] = ok ? r : NAN;
+            if (ok) {   // r >= 0: the bit patterns of non-negative doubles order like the values
+                const unsigned long long b = (unsigned long long)__double_as_longlong(r);
+                mine = b > mine ? b : mine;
+            }
+        }
+        __syncthreads();
+    }
+    atomicMax(&blk, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk) atomicMax(rmax_bits, blk);
+}
+
+// grid cell of every hull: edge 2 r_max + 1 (widened by a relative margin), so every pair that can
+// pass the test lies in neighbouring cells; cell coordinates wrap at 2^21 (aliasing only adds
+// candidates).  Key = (iz, iy, ix) with ix fastest: a cell row ix-1..ix+1 is one key range.
+__global__ __launch_bounds__(256) void key_kernel(int64_t n, const double* __restrict__ cx, const double* __restrict__ cy,
+                                                  const double* __restrict__ cz, const double* __restrict__ cr,
+                                                  const unsigned long long* __restrict__ rmax_bits,
+                                                  double* __restrict__ cell_out, uint64_t* __restrict__ keys,
+                                                  int32_t* __restrict__ idx) {
+    const double rmax = __longlong_as_double((long long)*rmax_bits);
+    const double cell = (2.0 * rmax + kTol) * (1.0 + 1e-9) + 1e-9;
+    for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < n; h += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t k = kInvalid;
+        if (!isnan(cr[h]))
+            k = cell_key((uint64_t)(int64_t)floor(cx[h] / cell), (uint64_t)(int64_t)floor(cy[h] / cell),
+                         (uint64_t)(int64_t)floor(cz[h] / cell));
+        keys[h] = k;
         idx[h] = (int32_t)h;
+        if (h == 0) *cell_out = cell;
     }
 }
 
 __global__ __launch_bounds__(256) void gather_kernel(int64_t n, const int32_t* __restrict__ order,
                                                      const double* __restrict__ cx, const double* __restrict__ cy,
                                                      const double* __restrict__ cz, const double* __restrict__ cr,
-                                                     const double* __restrict__ hi, double* __restrict__ sx,
-                                                     double* __restrict__ sy, double* __restrict__ sz,
-                                                     double* __restrict__ sr, double* __restrict__ shi) {
+                                                     double* __restrict__ sx, double* __restrict__ sy,
+                                                     double* __restrict__ sz, double* __restrict__ sr) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const int32_t h = order[p];
-        sx[p] = cx[h]; sy[p] = cy[h]; sz[p] = cz[h]; sr[p] = cr[h]; shi[p] = hi[h];
+        sx[p] = cx[h]; sy[p] = cy[h]; sz[p] = cz[h]; sr[p] = cr[h];
     }
 }
 
-// thread p: spheres q > p in x order while slo[q] <= shi[p]; EMIT = false counts, true writes keys
+DEV_BP int64_t lower_bound(const uint64_t* __restrict__ keys, int64_t n, uint64_t k) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t md = (lo + hi) >> 1;
+        if (keys[md] < k) lo = md + 1; else hi = md;
+    }
+    return lo;
+}
+
+// the hulls q of sorted positions with cell keys in [kl, kh] that form a passing pair with hull a
+// (larger index); returns how many, writing their keys from out[o] on when EMIT
 template <bool EMIT>
-__global__ __launch_bounds__(256) void sweep_kernel(int64_t n, const double* __restrict__ slo,
-                                                    const double* __restrict__ shi, const double* __restrict__ sx,
-                                                    const double* __restrict__ sy, const double* __restrict__ sz,
-                                                    const double* __restrict__ sr, const int32_t* __restrict__ order,
-                                                    int64_t* __restrict__ counts, const int64_t* __restrict__ offs,
-                                                    uint64_t* __restrict__ keys, int64_t max_pairs) {
+DEV_BP int64_t visit_range(uint64_t kl, uint64_t kh, int64_t n, const uint64_t* __restrict__ keys,
+                           const double* __restrict__ sx, const double* __restrict__ sy, const double* __restrict__ sz,
+                           const double* __restrict__ sr, const int32_t* __restrict__ order, int32_t a, double x,
+                           double y, double z, double r, uint64_t* __restrict__ out, int64_t o, int64_t max_pairs) {
+    int64_t c = 0;
+    for (int64_t q = lower_bound(keys, n, kl); q < n && keys[q] <= kh; ++q) {
+        const int32_t b = order[q];
+        if (b <= a) continue;
+        // NORM2(mp1 - mp2) <= r1 + r2 + TOL (:1185), mp1 = hull a
+        const double dx = x - sx[q], dy = y - sy[q], dz = z - sz[q];
+        if (!(::sqrt(dx * dx + dy * dy + dz * dz) <= r + sr[q] + kTol)) continue;
+        if constexpr (EMIT) {
+            if (o + c < max_pairs) out[o + c] = ((uint64_t)(uint32_t)a << 32) | (uint32_t)b;
+        }
+        ++c;
+    }
+    return c;
+}
+
+// thread p (cell-sorted hull): the hulls of the 27 neighbouring cells with a larger index that
+// pass the exact test; EMIT = false counts, true writes (a << 32 | b) keys at the thread's offset
+template <bool EMIT>
+__global__ __launch_bounds__(256) void grid_kernel(int64_t n, const uint64_t* __restrict__ keys,
+                                                   const double* __restrict__ sx, const double* __restrict__ sy,
+                                                   const double* __restrict__ sz, const double* __restrict__ sr,
+                                                   const int32_t* __restrict__ order, int64_t* __restrict__ counts,
+                                                   const int64_t* __restrict__ offs, uint64_t* __restrict__ out,
+                                                   int64_t max_pairs) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-        const double h = shi[p], x = sx[p], y = sy[p], z = sz[p], r = sr[p];
-        int64_t c = 0, o = EMIT ? offs[p] : 0;
-        const uint32_t a0 = EMIT ? (uint32_t)order[p] : 0u;
-        for (int64_t q = p + 1; q < n && slo[q] <= h; ++q) {
-            // NORM2(mp1 - mp2) <= r1 + r2 + TOL (:1185); symmetric bit for bit in (p, q)
-            const double dx = x - sx[q], dy = y - sy[q], dz = z - sz[q];
-            if (!(::sqrt(dx * dx + dy * dy + dz * dz) <= r + sr[q] + kTol)) continue;
-            if constexpr (EMIT) {
-                if (o + c < max_pairs) {
-                    const uint32_t b0 = (uint32_t)order[q];
-                    const uint32_t a = a0 < b0 ? a0 : b0, b = a0 < b0 ? b0 : a0;
-                    keys[o + c] = ((uint64_t)a << 32) | b;
+        const uint64_t k = keys[p];
+        int64_t c = 0;
+        if (k != kInvalid) {
+            const double x = sx[p], y = sy[p], z = sz[p], r = sr[p];
+            const int32_t a = order[p];
+            const int64_t o = EMIT ? offs[p] : 0;
+            const uint64_t ix = k & kMask, iy = (k >> 21) & kMask, iz = k >> 42;
+            const bool row = ix >= 1 && ix + 1 <= kMask;          // ix-1..ix+1 contiguous in key order
+            for (int t = 0; t < 9; ++t) {
+                const uint64_t jy = iy + (uint64_t)(t % 3) - 1, jz = iz + (uint64_t)(t / 3) - 1;
+                if (row) {
+                    c += visit_range<EMIT>(cell_key(ix - 1, jy, jz), cell_key(ix + 1, jy, jz), n, keys, sx, sy, sz, sr,
+                                           order, a, x, y, z, r, out, o + c, max_pairs);
+                } else {   // the row wraps at 2^21: its three cells separately
+                    for (uint64_t jx = ix - 1; jx != ix + 2; ++jx) {
+                        const uint64_t kc = cell_key(jx, jy, jz);
+                        c += visit_range<EMIT>(kc, kc, n, keys, sx, sy, sz, sr, order, a, x, y, z, r, out, o + c,
+                                               max_pairs);
+                    }
                 }
             }
-            ++c;
         }
         if constexpr (!EMIT) counts[p] = c;
     }
@@ -131,14 +227,14 @@ constexpr size_t kAlign = 256;
 size_t up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
-    size_t cx, cy, cz, cr, lo, hi, idx, slo, order, sx, sy, sz, sr, shi, counts, offs, keys, keys2, temp, total;
+    size_t cx, cy, cz, cr, rmax, cell, keys0, idx, skeys, order, sx, sy, sz, sr, counts, offs, pk, pk2, temp, total;
     size_t sort1, scan, sort2;
 };
 
 hipError_t temp_sizes(int64_t n, int64_t max_pairs, size_t& sort1, size_t& scan, size_t& sort2) {
     hipError_t e;
     sort1 = scan = sort2 = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort1, (const double*)nullptr, (double*)nullptr,
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort1, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                                 (const int32_t*)nullptr, (int32_t*)nullptr, (int)n)) != hipSuccess)
         return e;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int64_t*)nullptr, (int64_t*)nullptr, (int)(n + 1))) != hipSuccess)
@@ -151,11 +247,11 @@ Layout layout(int64_t n, int64_t max_pairs, size_t sort1, size_t scan, size_t so
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t at = o; o += up(bytes); return at; };
     const size_t d = (size_t)n * 8, i = (size_t)n * 4;
-    L.cx = take(d); L.cy = take(d); L.cz = take(d); L.cr = take(d); L.lo = take(d); L.hi = take(d);
-    L.idx = take(i); L.slo = take(d); L.order = take(i);
-    L.sx = take(d); L.sy = take(d); L.sz = take(d); L.sr = take(d); L.shi = take(d);
+    L.cx = take(d); L.cy = take(d); L.cz = take(d); L.cr = take(d); L.rmax = take(8); L.cell = take(8);
+    L.keys0 = take(d); L.idx = take(i); L.skeys = take(d); L.order = take(i);
+    L.sx = take(d); L.sy = take(d); L.sz = take(d); L.sr = take(d);
     L.counts = take((size_t)(n + 1) * 8); L.offs = take((size_t)(n + 1) * 8);
-    L.keys = take((size_t)max_pairs * 8); L.keys2 = take((size_t)max_pairs * 8);
+    L.pk = take((size_t)max_pairs * 8); L.pk2 = take((size_t)max_pairs * 8);
     L.sort1 = sort1; L.scan = scan; L.sort2 = sort2;
     L.temp = take(std::max(sort1, std::max(scan, sort2)));
     L.total = o;
@@ -188,28 +284,31 @@ hipError_t gjkepa_enqueue_broadphase(int vert_dtype, const void* verts, const in
     *ws_too_small = (int64_t)L.total > ws_bytes;
     if (*ws_too_small) return hipSuccess;
     const int nb = blocks_for(n);
+    if ((e = hipMemsetAsync(at<void>(ws, L.rmax), 0, 8, s)) != hipSuccess) return e;
+    auto* rmax = at<unsigned long long>(ws, L.rmax);
+    const int nbs = blocks_for((n + SPHERE_BLOCK / SG - 1) / (SPHERE_BLOCK / SG) * 256);   // one block per SPHERE_BLOCK / SG hulls
     if (vert_dtype == GJKEPA_DTYPE_F32)
-        hipLaunchKernelGGL(sphere_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)verts, hull_off, hull_cnt, n,
-                           at<double>(ws, L.cx), at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr),
-                           at<double>(ws, L.lo), at<double>(ws, L.hi), at<int32_t>(ws, L.idx));
+        hipLaunchKernelGGL(sphere_kernel<float>, dim3(nbs), dim3(SPHERE_BLOCK), 0, s, (const float*)verts, hull_off, hull_cnt, n,
+                           at<double>(ws, L.cx), at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr), rmax);
     else
-        hipLaunchKernelGGL(sphere_kernel<double>, dim3(nb), dim3(256), 0, s, (const double*)verts, hull_off, hull_cnt, n,
-                           at<double>(ws, L.cx), at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr),
-                           at<double>(ws, L.lo), at<double>(ws, L.hi), at<int32_t>(ws, L.idx));
+        hipLaunchKernelGGL(sphere_kernel<double>, dim3(nbs), dim3(SPHERE_BLOCK), 0, s, (const double*)verts, hull_off, hull_cnt, n,
+                           at<double>(ws, L.cx), at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr), rmax);
+    hipLaunchKernelGGL(key_kernel, dim3(nb), dim3(256), 0, s, n, at<double>(ws, L.cx), at<double>(ws, L.cy),
+                       at<double>(ws, L.cz), at<double>(ws, L.cr), (const unsigned long long*)rmax, at<double>(ws, L.cell),
+                       at<uint64_t>(ws, L.keys0), at<int32_t>(ws, L.idx));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t tb = L.sort1;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(at<void>(ws, L.temp), tb, at<double>(ws, L.lo), at<double>(ws, L.slo),
-                                                at<int32_t>(ws, L.idx), at<int32_t>(ws, L.order), (int)n, 0, 64, s)) != hipSuccess)
+    if ((e = hipcub::DeviceRadixSort::SortPairs(at<void>(ws, L.temp), tb, at<uint64_t>(ws, L.keys0),
+                                                at<uint64_t>(ws, L.skeys), at<int32_t>(ws, L.idx),
+                                                at<int32_t>(ws, L.order), (int)n, 0, 64, s)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(gather_kernel, dim3(nb), dim3(256), 0, s, n, at<int32_t>(ws, L.order), at<double>(ws, L.cx),
-                       at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr), at<double>(ws, L.hi),
-                       at<double>(ws, L.sx), at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr),
-                       at<double>(ws, L.shi));
+                       at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr), at<double>(ws, L.sx),
+                       at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr));
     if ((e = hipMemsetAsync(at<int64_t>(ws, L.counts) + n, 0, 8, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(sweep_kernel<false>, dim3(nb), dim3(256), 0, s, n, at<double>(ws, L.slo), at<double>(ws, L.shi),
-                       at<double>(ws, L.sx), at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr),
-                       at<int32_t>(ws, L.order), at<int64_t>(ws, L.counts), (const int64_t*)nullptr, (uint64_t*)nullptr,
-                       max_pairs);
+    hipLaunchKernelGGL(grid_kernel<false>, dim3(nb), dim3(256), 0, s, n, at<uint64_t>(ws, L.skeys), at<double>(ws, L.sx),
+                       at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr), at<int32_t>(ws, L.order),
+                       at<int64_t>(ws, L.counts), (const int64_t*)nullptr, (uint64_t*)nullptr, max_pairs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     tb = L.scan;
     if ((e = hipcub::DeviceScan::ExclusiveSum(at<void>(ws, L.temp), tb, at<int64_t>(ws, L.counts),
@@ -217,17 +316,16 @@ hipError_t gjkepa_enqueue_broadphase(int vert_dtype, const void* verts, const in
         return e;
     hipLaunchKernelGGL(total_kernel, dim3(1), dim3(64), 0, s, at<int64_t>(ws, L.offs), n, n_pairs);
     if (max_pairs > 0) {
-        if ((e = hipMemsetAsync(at<uint64_t>(ws, L.keys), 0xFF, (size_t)max_pairs * 8, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(sweep_kernel<true>, dim3(nb), dim3(256), 0, s, n, at<double>(ws, L.slo), at<double>(ws, L.shi),
-                           at<double>(ws, L.sx), at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr),
-                           at<int32_t>(ws, L.order), (int64_t*)nullptr, at<int64_t>(ws, L.offs), at<uint64_t>(ws, L.keys),
-                           max_pairs);
+        if ((e = hipMemsetAsync(at<uint64_t>(ws, L.pk), 0xFF, (size_t)max_pairs * 8, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(grid_kernel<true>, dim3(nb), dim3(256), 0, s, n, at<uint64_t>(ws, L.skeys), at<double>(ws, L.sx),
+                           at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr), at<int32_t>(ws, L.order),
+                           (int64_t*)nullptr, at<int64_t>(ws, L.offs), at<uint64_t>(ws, L.pk), max_pairs);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tb = L.sort2;
-        if ((e = hipcub::DeviceRadixSort::SortKeys(at<void>(ws, L.temp), tb, at<uint64_t>(ws, L.keys),
-                                                   at<uint64_t>(ws, L.keys2), (int)max_pairs, 0, 64, s)) != hipSuccess)
+        if ((e = hipcub::DeviceRadixSort::SortKeys(at<void>(ws, L.temp), tb, at<uint64_t>(ws, L.pk),
+                                                   at<uint64_t>(ws, L.pk2), (int)max_pairs, 0, 64, s)) != hipSuccess)
             return e;
-        hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(max_pairs)), dim3(256), 0, s, at<uint64_t>(ws, L.keys2),
+        hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(max_pairs)), dim3(256), 0, s, at<uint64_t>(ws, L.pk2),
                            (const int64_t*)n_pairs, max_pairs, pairs);
     }
     return hipGetLastError();
