@@ -8,6 +8,7 @@
 // follow the same pattern for the batched convex-hull kernels (two tiers over one cloud list).
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -18,6 +19,7 @@
 #include "gjkepa_kernel.h"
 #include "hull_kernel.h"
 #include "broadphase_kernel.h"
+#include "contacts_kernel.h"
 
 namespace {
 
@@ -451,6 +453,35 @@ int gjkepa_broadphase(int32_t vert_dtype, const void* verts, int64_t n_vert_scal
                   (e = hipStreamSynchronize(s)) != hipSuccess))
         return hip_fail(e, "hipMemcpyAsync D2H");
     return 0;
+}
+
+// ---- contact-list compaction (include/gjkepa.h) ---------------------
+int64_t gjkepa_compact_workspace_bytes(int64_t n_pairs) {
+    if (n_pairs < 0 || n_pairs > INT32_MAX) return GJKEPA_E_ARG;
+    const int64_t b = gjkepa_compact_ws_bytes(n_pairs);
+    return b < 0 ? fail(GJKEPA_E_NODEVICE, "workspace query needs a HIP device") : b;
+}
+
+int gjkepa_compact_hits_device(int32_t precision, const void* records, int64_t n_pairs, int32_t* hit_idx, void* hits,
+                               int64_t* n_hits, void* workspace, int64_t workspace_bytes, void* stream) {
+    if (n_pairs < 0 || n_pairs > INT32_MAX || (precision != GJKEPA_PREC_F32 && precision != GJKEPA_PREC_F64))
+        return fail(GJKEPA_E_ARG, "bad n_pairs/precision");
+    if (!n_hits) return fail(GJKEPA_E_ARG, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    if (n_pairs == 0) {
+        e = hipMemsetAsync(n_hits, 0, 8, s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    if (!records || !hit_idx || !workspace) return fail(GJKEPA_E_ARG, "null pointer");
+    const int64_t need = gjkepa_compact_ws_bytes(n_pairs);
+    if (need < 0) return fail(GJKEPA_E_HIP, "workspace query failed");
+    if (workspace_bytes < need) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
+    const int rb = gjkepa_record_bytes(precision);
+    const int flag = precision == GJKEPA_PREC_F64 ? (int)offsetof(gjkepa_contact_f64, collision)
+                                                  : (int)offsetof(gjkepa_contact_f32, collision);
+    e = gjkepa_enqueue_compact(records, n_pairs, rb, flag, hit_idx, hits, n_hits, workspace, s);
+    return e == hipSuccess ? 0 : hip_fail(e, "compaction launch");
 }
 
 }  // extern "C"

@@ -32,6 +32,7 @@ EXPORTS = (
     "gjkepa_batch_device", "gjkepa_last_error", "gjkepa_version_string", "gjkepa_synth_pairs",
     "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
     "gjkepa_broadphase_workspace_bytes", "gjkepa_broadphase", "gjkepa_broadphase_device", "gjkepa_synth_scene",
+    "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device",
 )
 HULL_MAX_POINTS = 256
 
@@ -108,6 +109,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_broadphase_device.restype = ctypes.c_int
     lib.gjkepa_synth_scene.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_i32, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp]
     lib.gjkepa_synth_scene.restype = c_i64
+    lib.gjkepa_compact_workspace_bytes.argtypes = [c_i64]
+    lib.gjkepa_compact_workspace_bytes.restype = c_i64
+    lib.gjkepa_compact_hits_device.argtypes = [c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]
+    lib.gjkepa_compact_hits_device.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -401,3 +406,17 @@ def broadphase_device(vert_dtype: int, verts_ptr: int, hull_off_ptr: int, hull_c
     rc = load().gjkepa_broadphase_device(int(vert_dtype), verts_ptr, hull_off_ptr, hull_cnt_ptr, int(n_hulls),
                                          pairs_ptr, int(max_pairs), n_pairs_ptr, ws_ptr, int(ws_bytes), stream or None)
     _check(rc, "gjkepa_broadphase_device")
+
+
+# ---- contact-list compaction ----------------------------------------
+def compact_workspace_bytes(n_pairs: int) -> int:
+    return int(load().gjkepa_compact_workspace_bytes(n_pairs))
+
+
+def compact_hits_device(precision: int, records_ptr: int, n_pairs: int, hit_idx_ptr: int, hits_ptr: int,
+                        n_hits_ptr: int, ws_ptr: int, ws_bytes: int, stream: int = 0) -> None:
+    """Dense, order-preserving list of the hit pairs of a device-resident batch (indices, and the
+    records when hits_ptr is non-zero); *n_hits is a device int64."""
+    rc = load().gjkepa_compact_hits_device(int(precision), records_ptr, int(n_pairs), hit_idx_ptr, hits_ptr or None,
+                                           n_hits_ptr, ws_ptr, int(ws_bytes), stream or None)
+    _check(rc, "gjkepa_compact_hits_device")

@@ -223,6 +223,17 @@ int gjkepa_broadphase_device(int32_t vert_dtype, const void* verts, const int64_
                              int32_t* pairs, int64_t max_pairs, int64_t* n_pairs,
                              void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- contact-list compaction -------------------------------------
+ * Turns a batch's records (gjkepa_batch_device output, one per pair) into the dense list a device
+ * consumer needs: hit_idx[k] = index of the k-th pair whose collision flag is set (ascending), and,
+ * when `hits` is not NULL, that pair's record copied to hits[k].  *n_hits (device int64) = count.
+ * Deterministic (no atomics), asynchronous on `stream`, graph-capturable; records stay in HBM.
+ * workspace: gjkepa_compact_workspace_bytes(n_pairs) bytes (tile counts, offsets, scan scratch). */
+int64_t gjkepa_compact_workspace_bytes(int64_t n_pairs);
+int gjkepa_compact_hits_device(int32_t precision, const void* records, int64_t n_pairs,
+                               int32_t* hit_idx, void* hits, int64_t* n_hits,
+                               void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Last error message of the calling thread ("" if none). */
 const char* gjkepa_last_error(void);
 
