@@ -5,8 +5,10 @@ Workload (N=1) = BASELINE config C2: 2^20 random 32-vertex convex-hull pairs, fp
 version_=2, TOL_FF_=1.0, hull B centre offset r ~ U[0, 2.5] (seed 0x6A4B5C1D).
 A "step" is one pass of the hot path (gjkepa_batch_device: the tiered GJK/EPA kernels) over the
 whole batch, with hulls, pair list and output already resident in HBM.  For N > 1 each rank owns
-a contiguous shard of `--pairs-per-gpu` pairs (weak scaling) and every step ends with an RCCL
-all-gather of the contact records over xGMI (config C3's exchange).
+a contiguous shard of `--pairs-per-gpu` pairs (weak scaling) and every step's contact records are
+all-gathered over xGMI with RCCL (config C3's exchange).  The gather of step i runs on RCCL's
+stream while step i+1's kernels run (two record buffers); the timed region ends after the last
+gather has completed, so every step's exchange is inside it (`--no-overlap`: gather in line).
 
 Extra legs (not timed in `value`): the roofline of the dominant kernel from HIP events on the
 launch stream, and on rank 0 at N=1 a CPU baseline — the oracle restatement (kind "port") over a
@@ -58,6 +60,8 @@ def parse():
     ap.add_argument("--version", type=int, default=2)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather for N>1")
+    ap.add_argument("--no-overlap", action="store_true", help="N>1: gather synchronously instead of overlapping it "
+                                                                "with the next step's kernels")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
     ap.add_argument("--cpu-sample", type=int, default=0, help="pairs for the CPU baseline (0: the whole batch)")
@@ -102,33 +106,53 @@ def main():
     ws_bytes = gjkepa.workspace_bytes(n)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
     gathered = None
+    # RCCL path: two record buffers; step i's all-gather (RCCL's own stream) overlaps step i+1's
+    # kernels, and a buffer is rewritten only after the gather that read it has finished
+    overlap = world > 1 and not args.no_gather and not host_coll and not args.no_overlap
+    outs = [out, torch.zeros_like(out)] if overlap else [out]
     if world > 1 and not args.no_gather:
-        gathered = torch.empty(world * n * rec_bytes, dtype=torch.uint8, device=dev)
+        gathered = [torch.empty(world * n * rec_bytes, dtype=torch.uint8, device=dev) for _ in outs]
+    works = [None] * len(outs)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    def launch(p):
+    def launch(p, o):
         gjkepa.gjkepa_batch_device(args.version, 1.0, gjkepa.DTYPE_F32, p, verts.data_ptr(), off.data_ptr(),
-                                   cnt.data_ptr(), prs.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes, sptr)
+                                   cnt.data_ptr(), prs.data_ptr(), n, o.data_ptr(), ws.data_ptr(), ws_bytes, sptr)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    nstep = [0]
 
     def step(i=None):
+        b = nstep[0] % len(outs)
+        nstep[0] += 1
+        if works[b] is not None:
+            works[b].wait()             # the compute stream waits for the gather that read outs[b]
+            works[b] = None
         if i is not None:
             ev[i][0].record(stream)
-        launch(prec)
+        launch(prec, outs[b])
         if i is not None:
             ev[i][1].record(stream)
         if gathered is not None:
             if host_coll:
                 g = torch.empty(world * n * rec_bytes, dtype=torch.uint8)
-                dist.all_gather_into_tensor(g, out.cpu())
-                gathered.copy_(g)
+                dist.all_gather_into_tensor(g, outs[b].cpu())
+                gathered[b].copy_(g)
+            elif overlap:
+                works[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
             else:
-                dist.all_gather_into_tensor(gathered, out)
+                dist.all_gather_into_tensor(gathered[b], outs[b])
+
+    def drain():
+        for k, w in enumerate(works):
+            if w is not None:
+                w.wait()
+                works[k] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -136,6 +160,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    drain()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -151,7 +176,7 @@ def main():
     value = total_pairs * args.steps / elapsed / 1e6
 
     # statistics of the last step's records (rank-local)
-    recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
+    recs = np.frombuffer(outs[(nstep[0] - 1) % len(outs)].cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
     hit_rate = float((recs["collision"] != 0).mean())
     status_counts = {int(k): int(v) for k, v in zip(*np.unique(recs["status"], return_counts=True))}
     epa_iters = (recs["diag"] >> 8) & 0xFF
@@ -189,7 +214,8 @@ def main():
                                f"version_={args.version}, TOL_FF_=1.0, hull B offset r~U[0,{rmax}]",
                    "hull_vertices": [nmin, nmax],
                    "pairs_per_gpu": n, "total_pairs": total_pairs, "seed": SEED,
-                   "parallelism": f"shard{world}" + ("+allgather" if gathered is not None else ""),
+                   "parallelism": f"shard{world}" + ("" if gathered is None else "+allgather_overlapped" if overlap
+                                                       else "+allgather"),
                    "vert_storage": "f32", "record_bytes": rec_bytes},
         "roofline": roofline,
         "hit_rate": round(hit_rate, 4), "epa_iters_mean": round(epa_mean, 2), "status_counts": status_counts,
