@@ -1,6 +1,7 @@
 #!/bin/bash
-# Build a variant of libgjkepa_hip.so with overridden tier parameters (for A/B timing).
-# usage: tools/build_variant.sh NAME "-DGJKEPA_T0_G=32 -DGJKEPA_T0_K=1 ..."
+# Build a variant of libgjkepa_hip.so with overridden tier parameters (for A/B timing).  Only the
+# narrow-phase kernels and the C-ABI are rebuilt; the other kernel objects come from build/.
+# usage: tools/build_variant.sh NAME "-DGJKEPA_E0_MINW=3 ..."
 set -e
 NAME=$1; shift
 D=collision-detect-gjk-epa_amd
@@ -9,5 +10,6 @@ mkdir -p $OUT
 F="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $*"
 /opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_kernel.hip -o $OUT/k.o
 /opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_capi.cpp -o $OUT/c.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k.o $OUT/c.o $D/build/synth.o -o $OUT/libgjkepa_hip.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k.o $OUT/c.o $D/build/hull_kernel.o \
+    $D/build/broadphase_kernel.o $D/build/contacts_kernel.o $D/build/synth.o -o $OUT/libgjkepa_hip.so
 echo built $OUT/libgjkepa_hip.so
