@@ -3,8 +3,8 @@
 // Host-buffer entries (gjkepa_query, gjkepa_batch) own per-device staging buffers that grow as
 // needed and are reused; they are serialised per device by a mutex, so concurrent callers (the
 // reference's `!$OMP PARALLEL DO ... CALL GJKEPA` pattern) are safe.  gjkepa_batch_device never
-// allocates or synchronises: it enqueues a 64-byte counter reset and eight kernels (2 GJK + 4 EPA +
-// 2 contact tiers); each kernel takes 64-pair chunks from its own counter.  gjkepa_hull_batch(_device)
+// allocates or synchronises: it enqueues a 256-byte counter / tally reset and nine kernels (2 GJK +
+// 5 EPA + 2 contact tiers); each kernel takes 64-pair chunks (or runs of 16) from its own counter.  gjkepa_hull_batch(_device)
 // follow the same pattern for the batched convex-hull kernels (two tiers over one cloud list).
 #include <hip/hip_runtime.h>
 
@@ -34,7 +34,10 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 constexpr int64_t kWsHeader = 256;
-constexpr int kSparseClaim = 16;   // tiers that serve few pairs claim runs of 16 chunks (one 1-KB route load)
+constexpr int kSparseClaim = 16;
+#ifndef GJKEPA_DENSE_EPA_TIERS
+#define GJKEPA_DENSE_EPA_TIERS 2   // EPA tiers below this always claim single chunks; the others start
+#endif                             // sparse and switch to single chunks when their route tally is dense   // tiers that serve few pairs claim runs of 16 chunks (one 1-KB route load)
 
 struct DevBuf {
     void* p = nullptr;
@@ -88,13 +91,15 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus) {
     if (n_pairs == 0) return 0;
     if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
-    // workspace: per-launch chunk counters (zeroed here), then one route byte per pair (written by
-    // GJK tier 0 for every pair before any read)
+    // workspace: per-launch chunk counters and route tallies (zeroed here), then one route byte per
+    // pair (written by GJK tier 0 for every pair before any read)
     uint32_t* ctr = (uint32_t*)workspace;
     uint8_t* route = (uint8_t*)workspace + kWsHeader;
     hipError_t e;
-    if ((e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * GJKEPA_WS_COUNTERS, s)) != hipSuccess)
+    static_assert(sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY) <= kWsHeader, "workspace header");
+    if ((e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY), s)) != hipSuccess)
         return hip_fail(e, "workspace counter reset");
+    uint32_t* tally = ctr + GJKEPA_WS_COUNTERS;
     int launch = 0;
     gjkepa_gjk_args g{};
     g.verts = verts;
@@ -103,6 +108,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     g.pairs = pairs;
     g.n_pairs = n_pairs;
     g.route = route;
+    g.tally = tally;
     g.out = out;
     g.num_cus = num_cus;
     g.route_code = -1;                                   // GJK tier 0: every pair
@@ -122,13 +128,14 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.pairs = pairs;
     a.n_pairs = n_pairs;
     a.route = route;
+    a.tally = tally;
     a.out = out;
     a.num_cus = num_cus;
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {          // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
         a.ctr = ctr + launch++;
-        a.claim = t <= 1 ? 1 : kSparseClaim;
+        a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
         if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, s)) != hipSuccess) return hip_fail(e, "EPA tier launch");
     }
     for (int t = 0; t < GJKEPA_CONTACT_TIERS; ++t) {      // contact features of every EPA result
@@ -177,15 +184,16 @@ int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
 const char* gjkepa_last_error(void) { return g_err.c_str(); }
 
 const char* gjkepa_version_string(void) {
-    static char buf[512];
+    static char buf[640];
     std::snprintf(buf, sizeof(buf),
                   "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
-                  "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
+                  "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
                   "-O3 -ffp-contract=off",
                   GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
                   GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP,
-                  GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G, GJKEPA_C1_K);
+                  GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
+                  GJKEPA_C1_K);
     return buf;
 }
 

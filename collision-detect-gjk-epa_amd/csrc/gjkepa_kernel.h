@@ -63,19 +63,19 @@
 #define GJKEPA_E1_MINW 2
 #endif
 #ifndef GJKEPA_E2_G
-#define GJKEPA_E2_G 64
+#define GJKEPA_E2_G 32          // two pairs per wave for hulls of 33-128 vertices (configs C4, C5)
 #endif
 #ifndef GJKEPA_E2_K
 #define GJKEPA_E2_K 4
 #endif
 #ifndef GJKEPA_E2_VCAP
-#define GJKEPA_E2_VCAP 104
+#define GJKEPA_E2_VCAP 72       // polytope overflow goes on to tier 3 (A/B: 104 / 208 spills at 2 waves)
 #endif
 #ifndef GJKEPA_E2_FCAP
-#define GJKEPA_E2_FCAP 208
+#define GJKEPA_E2_FCAP 128
 #endif
 #ifndef GJKEPA_E2_MINW
-#define GJKEPA_E2_MINW 1
+#define GJKEPA_E2_MINW 2
 #endif
 #ifndef GJKEPA_E3_G
 #define GJKEPA_E3_G 64
@@ -84,13 +84,28 @@
 #define GJKEPA_E3_K 4
 #endif
 #ifndef GJKEPA_E3_VCAP
-#define GJKEPA_E3_VCAP 208
+#define GJKEPA_E3_VCAP 104
 #endif
 #ifndef GJKEPA_E3_FCAP
-#define GJKEPA_E3_FCAP 416
+#define GJKEPA_E3_FCAP 208
 #endif
 #ifndef GJKEPA_E3_MINW
 #define GJKEPA_E3_MINW 1
+#endif
+#ifndef GJKEPA_E4_G
+#define GJKEPA_E4_G 64
+#endif
+#ifndef GJKEPA_E4_K
+#define GJKEPA_E4_K 4
+#endif
+#ifndef GJKEPA_E4_VCAP
+#define GJKEPA_E4_VCAP 208
+#endif
+#ifndef GJKEPA_E4_FCAP
+#define GJKEPA_E4_FCAP 416
+#endif
+#ifndef GJKEPA_E4_MINW
+#define GJKEPA_E4_MINW 1
 #endif
 // contact-feature tiers (nearest points, contact point, contact type): G, K as above
 #ifndef GJKEPA_C0_G
@@ -106,11 +121,15 @@
 #define GJKEPA_C1_K 4
 #define GJKEPA_C1_MINW 1
 #define GJKEPA_GJK_TIERS 2
-#define GJKEPA_EPA_TIERS 4
+#define GJKEPA_EPA_TIERS 5
 #define GJKEPA_CONTACT_TIERS 2
 
 // workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair
-#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (8 launches used)
+#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (9 launches used)
+// then GJKEPA_WS_TALLY uint32 route tallies (indexed by route code): every kernel adds the pairs it
+// routes on; a launch whose own tally is at least 1/16 of the batch claims single chunks (dense),
+// otherwise runs of `claim` chunks (sparse scan)
+#define GJKEPA_WS_TALLY 48
 // route byte per pair (workspace): which kernel owns the pair next
 #define GJKEPA_ROUTE_DONE 0
 #define GJKEPA_ROUTE_GJK1 1
@@ -126,7 +145,8 @@ struct gjkepa_gjk_args {
     uint8_t* route;             // [n_pairs]
     int route_code;             // pairs this launch serves: -1 = all (tier 0), else route code
     uint32_t* ctr;              // this launch's chunk counter (zero at launch)
-    int claim;                  // 64-pair chunks taken per counter increment
+    int claim;                  // 64-pair chunks taken per counter increment (sparse default)
+    uint32_t* tally;            // pairs routed to each route code so far (GJKEPA_WS_TALLY entries)
     void* out;                  // contact records (hits: simplex codes parked in their slot)
     int grid;                   // <= 0: occupancy x CUs
     int num_cus;
@@ -144,7 +164,8 @@ struct gjkepa_epa_args {
     int route_code;             // GJKEPA_ROUTE_EPA0 + tier
     int next_code;              // route code for polytope overflow; -1 on the last tier
     uint32_t* ctr;              // this launch's chunk counter (zero at launch)
-    int claim;                  // 64-pair chunks taken per counter increment
+    int claim;                  // 64-pair chunks taken per counter increment (sparse default)
+    uint32_t* tally;            // pairs routed to each route code so far (GJKEPA_WS_TALLY entries)
     void* out;
     int grid;
     int num_cus;

@@ -1295,9 +1295,9 @@ template <int G, typename T> DEV void store_record(void* out, int64_t pair, int 
 // hull capacity (vertices) of EPA tier t
 DEV constexpr int epa_hull_cap(int t) {
     return t == 0 ? GJKEPA_E0_G * GJKEPA_E0_K : t == 1 ? GJKEPA_E1_G * GJKEPA_E1_K : t == 2 ? GJKEPA_E2_G * GJKEPA_E2_K
-                                                                                        : GJKEPA_E3_G * GJKEPA_E3_K;
+         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : GJKEPA_E4_G * GJKEPA_E4_K;
 }
-static_assert(GJKEPA_E3_G * GJKEPA_E3_K >= GJKEPA_MAX_HULL_VERTS, "the last EPA tier must hold every hull");
+static_assert(GJKEPA_E4_G * GJKEPA_E4_K >= GJKEPA_MAX_HULL_VERTS, "the last EPA tier must hold every hull");
 // smallest EPA tier >= t0 whose hull capacity holds nmax vertices
 DEV int epa_tier_for(int nmax, int t0 = 0) {
     for (int t = t0; t < GJKEPA_EPA_TIERS - 1; ++t)
@@ -1350,6 +1350,27 @@ template <int SMALL> struct Units {
         if (p0 + len > n_pairs) len = (int)(n_pairs - p0);
     }
 };
+
+// Route tallies (workspace): each wave counts the pairs it routes per code in LDS and adds them to
+// the launch-wide tallies once at its end; a later launch reads its own code's tally to pick dense
+// (single-chunk claims) or sparse (runs of a.claim chunks) scheduling.
+__shared__ uint32_t s_tally[GJKEPA_WS_TALLY];
+DEV void tally_begin() {
+    if (lane_id() < GJKEPA_WS_TALLY) s_tally[lane_id()] = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+DEV void tally_route(uint8_t code) { if (code < GJKEPA_WS_TALLY) atomicAdd(&s_tally[code], 1u); }
+DEV void tally_end(uint32_t* tally) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    const int l = lane_id();
+    if (l < GJKEPA_WS_TALLY && s_tally[l]) atomicAdd(&tally[l], s_tally[l]);
+}
+DEV int pick_claim(const uint32_t* tally, int route_code, int64_t n_pairs, int claim) {
+    if (route_code < 0 || claim <= 1) return claim;
+    const uint32_t mine = __builtin_amdgcn_readfirstlane(tally[route_code]);
+    return (int64_t)mine * 16 >= n_pairs ? 1 : claim;
+}
 
 template <int G, typename F>
 DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code,
@@ -1421,7 +1442,9 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
+    tally_begin();
+    const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SG_ROUTE);
         Ctx<T, TIn, G, K, 0, 0> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1462,11 +1485,12 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                 }
             }
         }
-        if (gl == 0) a.route[pair] = next;
+        if (gl == 0) { a.route[pair] = next; tally_route(next); }
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SG_STORE);
     });
     GK_STAMP(SG_ROUTE);
+    tally_end(a.tally);
     GK_STAMP_END();
 }
 
@@ -1484,7 +1508,9 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
+    tally_begin();
+    const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, VC, FC> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1522,11 +1548,12 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
             for (int i = 0; i < 13; ++i) o13[i] = T(0);
             store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
         }
-        if (gl == 0) a.route[pair] = next;
+        if (gl == 0) { a.route[pair] = next; tally_route(next); }
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SE_STORE);
     });
     GK_STAMP(SE_ROUTE);
+    tally_end(a.tally);
     GK_STAMP_END();
 }
 
@@ -1585,6 +1612,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     const int gl = grp.gl;
     const int gid = grp.lane / G;
     const TIn* verts = (const TIn*)a.verts;
+    tally_begin();
     PairQueue<(2 * NG > 8 ? 2 * NG : 8)> q(a.route, a.n_pairs, a.route_code, a.ctr);
     Ctx<T, TIn, G, K, VC, FC> c{L, grp};
     EpaState<T, R> S;
@@ -1609,7 +1637,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             for (int i = 0; i < 13; ++i) o13[i] = T(0);
             store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
         }
-        if (gl == 0) a.route[pair] = next;
+        if (gl == 0) { a.route[pair] = next; tally_route(next); }
     };
     for (;;) {
         // refill idle groups (in group order) once enough of them are idle
@@ -1656,6 +1684,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             }
         }
     }
+    tally_end(a.tally);
 }
 
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
@@ -1669,7 +1698,9 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, a.claim, [&](int64_t pair) {
+    tally_begin();
+    const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, 0, 1> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1702,6 +1733,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
         GK_STAMP(SE_STORE);
     });
     GK_STAMP(SE_ROUTE);
+    tally_end(a.tally);
     GK_STAMP_END();
 }
 
@@ -1774,7 +1806,8 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
         case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
         case 1: return launch_epa<TIn, T, EPA_ARGS(1)>(a, s);
         case 2: return launch_epa<TIn, T, EPA_ARGS(2)>(a, s);
-        default: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
+        case 3: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
+        default: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
     }
 }
 
