@@ -25,9 +25,15 @@
 #ifndef GJKEPA_G0_MINW
 #define GJKEPA_G0_MINW 2        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
 #endif
-#define GJKEPA_G1_G 64
-#define GJKEPA_G1_K 4
+#ifndef GJKEPA_G1_G
+#define GJKEPA_G1_G 32          // two pairs per wave (A/B on C4: 26.3 vs 25.5M queries/s at 64 lanes x 4)
+#endif
+#ifndef GJKEPA_G1_K
+#define GJKEPA_G1_K 8
+#endif
+#ifndef GJKEPA_G1_MINW
 #define GJKEPA_G1_MINW 2
+#endif
 // EPA tiers: G, K as above, EPA polytope capacity VCAP vertices / FCAP faces
 #ifndef GJKEPA_E0_G
 #define GJKEPA_E0_G 16
@@ -77,6 +83,9 @@
 #ifndef GJKEPA_E2_MINW
 #define GJKEPA_E2_MINW 2
 #endif
+#ifndef GJKEPA_E2_REFILL
+#define GJKEPA_E2_REFILL 0
+#endif
 #ifndef GJKEPA_E3_G
 #define GJKEPA_E3_G 64
 #endif
@@ -117,9 +126,15 @@
 #ifndef GJKEPA_C0_MINW
 #define GJKEPA_C0_MINW 2
 #endif
+#ifndef GJKEPA_C1_G
 #define GJKEPA_C1_G 64
+#endif
+#ifndef GJKEPA_C1_K
 #define GJKEPA_C1_K 4
+#endif
+#ifndef GJKEPA_C1_MINW
 #define GJKEPA_C1_MINW 1
+#endif
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 5
 #define GJKEPA_CONTACT_TIERS 2

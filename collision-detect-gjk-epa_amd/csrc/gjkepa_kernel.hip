@@ -1805,7 +1805,7 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
         case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
         case 1: return launch_epa<TIn, T, EPA_ARGS(1)>(a, s);
-        case 2: return launch_epa<TIn, T, EPA_ARGS(2)>(a, s);
+        case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL>(a, s);
         case 3: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
         default: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
     }
