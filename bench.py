@@ -49,6 +49,20 @@ def algorithmic_bytes_per_query(mean_verts_per_pair: float, vert_bytes: int, rec
     return vert_bytes * 3 * mean_verts_per_pair + 2 * 4 + 2 * (8 + 4) + rec_bytes
 
 
+def moved_copy(pool, delta: float, seed: int) -> np.ndarray:
+    """The pool's vertices with hull B of every pair translated by a random vector of length delta."""
+    rng = np.random.default_rng(seed)
+    v = pool.verts.astype(np.float64).copy()
+    hb = pool.pairs[:, 1].astype(np.int64)
+    d = rng.normal(size=(len(hb), 3))
+    d *= delta / np.linalg.norm(d, axis=1, keepdims=True)
+    cnt = pool.hull_cnt[hb].astype(np.int64)
+    idx = np.repeat(pool.hull_off[hb], cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    for j in range(3):
+        v[idx + j * np.repeat(cnt, cnt)] += np.repeat(d[:, j], cnt)
+    return v.astype(pool.verts.dtype)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +78,7 @@ def parse():
                                                                 "with the next step's kernels")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
+    ap.add_argument("--no-warm-leg", action="store_true", help="skip the warm-start side measurement")
     ap.add_argument("--cpu-sample", type=int, default=0, help="pairs for the CPU baseline (0: the whole batch)")
     return ap.parse_args()
 
@@ -241,6 +256,36 @@ def main():
         r32 = np.frombuffer(out32.cpu().numpy().tobytes(), dtype=gjkepa.REC32)
         result["fp32_compute"] = {"value": round(n / (ms32 * 1e-3) / 1e6, 3), "unit": "M queries/s",
                                   "hit_agreement_vs_f64": round(float((r32["collision"] == recs["collision"]).mean()), 6)}
+
+    # warm start: frames alternate between the batch and a copy with every hull B moved
+    # by 1e-3; each frame's warm slots seed the next.  Cold = the same frames through batch_device.
+    if rank == 0 and world == 1 and not args.no_warm_leg and prec == gjkepa.PREC_F64:
+        moved = moved_copy(pool, 1e-3, SEED)
+        frames = [verts, torch.from_numpy(moved).to(dev)]
+        warm = torch.full((4 * n,), -1, dtype=torch.int32, device=dev)
+
+        def frame(i, use_warm):
+            args_ = (args.version, 1.0, gjkepa.DTYPE_F32, prec, frames[i % 2].data_ptr(), off.data_ptr(),
+                     cnt.data_ptr(), prs.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes)
+            if use_warm:
+                gjkepa.gjkepa_batch_warm_device(*args_, warm.data_ptr(), sptr)
+            else:
+                gjkepa.gjkepa_batch_device(*args_, sptr)
+        rates = {}
+        for use_warm in (False, True):
+            frame(0, use_warm)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for i in range(1, args.steps + 1):
+                frame(i, use_warm)
+            torch.cuda.synchronize(dev)
+            rates[use_warm] = n * args.steps / (time.perf_counter() - t) / 1e6
+        wr = np.frombuffer(out.cpu().numpy().tobytes(), dtype=gjkepa.REC64)
+        hits = (wr["collision"] != 0) & (wr["status"] == 0)
+        result["warm_start"] = {"value": round(rates[True], 3), "cold_value": round(rates[False], 3),
+                                "unit": "M queries/s", "warm_started_hits": round(float(((wr["diag"] & 0xFF) == 0)[hits].mean()), 4),
+                                "note": "frames alternate between the batch and hull B moved by 1e-3; "
+                                        "gjkepa_batch_warm_device vs gjkepa_batch_device on the same frames"}
 
     # host-buffer entry point (gjkepa_batch: H2D copy of hulls/pairs, kernels, D2H of records):
     # the PCIe-inclusive rate, reported beside `value`, never as it

@@ -88,7 +88,7 @@ int num_cus_current() {
 
 int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
-            void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus) {
+            void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus, uint32_t* warm = nullptr) {
     if (n_pairs == 0) return 0;
     if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
     // workspace: per-launch chunk counters and route tallies (zeroed here), then one route byte per
@@ -109,6 +109,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     g.n_pairs = n_pairs;
     g.route = route;
     g.tally = tally;
+    g.warm = warm;
     g.out = out;
     g.num_cus = num_cus;
     g.route_code = -1;                                   // GJK tier 0: every pair
@@ -207,6 +208,18 @@ int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int3
     if (n_pairs > INT32_MAX) return fail(GJKEPA_E_ARG, "n_pairs above 2^31-1");
     return enqueue(version, tol_ff, vert_dtype, precision, verts, hull_off, hull_cnt, pairs, n_pairs, out,
                    workspace, workspace_bytes, (hipStream_t)stream, num_cus_current());
+}
+
+int gjkepa_batch_warm_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                             const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                             const int32_t* pairs, int64_t n_pairs, void* out, void* workspace,
+                             int64_t workspace_bytes, uint32_t* warm, void* stream) {
+    if (n_pairs < 0 || !valid_enums(vert_dtype, precision)) return fail(GJKEPA_E_ARG, "bad n_pairs/dtype/precision");
+    if (n_pairs > 0 && (!verts || !hull_off || !hull_cnt || !pairs || !out || !workspace || !warm))
+        return fail(GJKEPA_E_ARG, "null pointer");
+    if (n_pairs > INT32_MAX) return fail(GJKEPA_E_ARG, "n_pairs above 2^31-1");
+    return enqueue(version, tol_ff, vert_dtype, precision, verts, hull_off, hull_cnt, pairs, n_pairs, out,
+                   workspace, workspace_bytes, (hipStream_t)stream, num_cus_current(), warm);
 }
 
 int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,

@@ -162,6 +162,7 @@ struct gjkepa_gjk_args {
     uint32_t* ctr;              // this launch's chunk counter (zero at launch)
     int claim;                  // 64-pair chunks taken per counter increment (sparse default)
     uint32_t* tally;            // pairs routed to each route code so far (GJKEPA_WS_TALLY entries)
+    uint32_t* warm;             // optional [4 * n_pairs] warm-start simplex codes (in / out)
     void* out;                  // contact records (hits: simplex codes parked in their slot)
     int grid;                   // <= 0: occupancy x CUs
     int num_cus;

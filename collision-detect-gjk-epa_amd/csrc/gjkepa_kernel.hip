@@ -1074,8 +1074,45 @@ CTX_T DEV void update_simplex_c(const CTX& c, V3<T> nq, V3<T>& s0, V3<T>& s1, V3
     k3 = km;
 }
 
+// Warm start: the simplex a previous call ended GJK with, as support codes
+// (ia | ib << 16).  Rebuilt from the current vertices; when the origin lies strictly inside it (every
+// face more than kWarmMargin from the origin, so the hulls certainly overlap and a flat or touching
+// tetrahedron never qualifies), the pair is a hit and EPA starts from it: GJK's iterations are
+// skipped.  Otherwise the call runs the reference GJK from scratch.  Results then agree with a cold
+// call to EPA's tolerance rather than bit for bit (a different start polytope).
+// A pair that missed is marked kWarmMiss; its next call first tries the axis between the hull
+// centres (the sphere test's means) and answers a miss when it separates the hulls by more than
+// kWarmMargin — the reference's own output for a miss (all zero), without GJK's iterations.
+constexpr double kWarmMargin = 1e-6;
+constexpr uint32_t kWarmMiss = 0xFFFFFFFEu;
+CTX_T DEV bool warm_start(CTX& c, const uint32_t* w, uint32_t* kc) {
+    uint32_t code[4];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        code[i] = w[i];
+        ok = ok && code[i] != kStale && (int)(code[i] & 0xffffu) < c.na && (int)(code[i] >> 16) < c.nb;
+    }
+    if (!c.g.unib(ok)) return false;
+    const V3<T> s0 = decode_pt(c, code[0]), s1 = decode_pt(c, code[1]), s2 = decode_pt(c, code[2]), s3 = decode_pt(c, code[3]);
+    const V3<T> M = centroid4(s0, s1, s2, s3), O = zero3<T>();
+    const V3<T> P[4] = {s0, s1, s2, s3};
+    const int F[4][3] = {{0, 2, 3}, {0, 1, 3}, {0, 1, 2}, {1, 2, 3}};
+    bool inside = true;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        V3<T> n = face_nml(P[F[f][0]], P[F[f][1]], P[F[f][2]]);
+        if (dot(n, vsub(P[F[f][0]], M)) < T(0)) n = vneg(n);
+        inside = inside && dot(vsub(P[F[f][0]], O), n) > T(kWarmMargin);
+    }
+    if (!c.g.unib(inside)) return false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kc[i] = code[i];
+    return true;
+}
+
 // Sphere pre-test + GJK.  Returns PH_MISS, PH_HIT (codes k0..k3 filled) or an error status.
-CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
+CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false) {
     const V3<T> O = zero3<T>();
     auto& L = c.L;
     const int gl = c.g.gl;
@@ -1121,6 +1158,21 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it) {
         r2 = tsqrt(gmax<G>(r2));
         GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
+        if (try_axis) {   // warm start, pair missed last call: the centre axis separates the hulls
+            const V3<T> d = vsub(m2, m1);
+            T amax = -Tol<T>::BIG, bmin = Tol<T>::BIG;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = k * G + gl;
+                const T ta = d.x * c.ax[k] + d.y * c.ay[k] + d.z * c.az[k];
+                const T tb = d.x * c.bx[k] + d.y * c.by[k] + d.z * c.bz[k];
+                if (i < c.na && ta > amax) amax = ta;
+                if (i < c.nb && tb < bmin) bmin = tb;
+            }
+            amax = gmax<G>(amax);
+            bmin = gmin<G>(bmin);
+            if (c.g.unib(bmin - amax > T(kWarmMargin) * norm2(d))) return PH_MISS;
+        }
     }
     // --- initial simplex (:82-170)
     V3<T> s0 = O, s1 = O, s2 = O, s3 = O;   // fresh SAVE state: stale row 4 = 0
@@ -1455,6 +1507,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         uint8_t next = 0;
         if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
             store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+            if (a.warm && gl < 4) a.warm[4 * pair + gl] = kStale;
         } else if (na > K * G || nb > K * G) {
             next = GJKEPA_ROUTE_GJK1;                        // larger GJK tier
         } else {
@@ -1464,12 +1517,23 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
             GK_STAMP(SG_LOAD);
             if (bad_in) {
                 store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+                if (a.warm && gl < 4) a.warm[4 * pair + gl] = kStale;
             } else {
                 uint32_t kc[4];
                 int gjk_it = 0;
-                const int r = gjk_phase(c, kc, gjk_it);
+                int r = PH_MISS;
+                bool warm_hit = false, try_axis = false;
+                if (a.warm) {
+                    try_axis = a.warm[4 * pair] == kWarmMiss;
+                    if (!try_axis) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
+                }
+                if (warm_hit) r = PH_HIT;
+                else r = gjk_phase(c, kc, gjk_it, try_axis);
                 __builtin_amdgcn_wave_barrier();
                 GK_STAMP(SG_CHK);
+                if (a.warm && gl < 4)   // this call's simplex seeds the next call; a miss mark; none for errors
+                    a.warm[4 * pair + gl] = r == PH_HIT ? (gl == 0 ? kc[0] : gl == 1 ? kc[1] : gl == 2 ? kc[2] : kc[3])
+                                          : (r == PH_MISS && gl == 0) ? kWarmMiss : kStale;
                 if (r == PH_HIT) {
 #pragma unroll
                     for (int j0 = 0; j0 < 5; j0 += G) {

@@ -32,7 +32,7 @@ EXPORTS = (
     "gjkepa_batch_device", "gjkepa_last_error", "gjkepa_version_string", "gjkepa_synth_pairs",
     "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
     "gjkepa_broadphase_workspace_bytes", "gjkepa_broadphase", "gjkepa_broadphase_device", "gjkepa_synth_scene",
-    "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device",
+    "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
 )
 HULL_MAX_POINTS = 256
 
@@ -113,6 +113,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_compact_workspace_bytes.restype = c_i64
     lib.gjkepa_compact_hits_device.argtypes = [c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]
     lib.gjkepa_compact_hits_device.restype = ctypes.c_int
+    lib.gjkepa_batch_warm_device.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                             c_vp, c_vp]
+    lib.gjkepa_batch_warm_device.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -243,6 +246,18 @@ def gjkepa_batch_device(version: int, tol_ff: float, vert_dtype: int, precision:
                                     hull_off_ptr, hull_cnt_ptr, pairs_ptr, int(n_pairs), out_ptr, ws_ptr,
                                     int(ws_bytes), stream or None)
     _check(rc, "gjkepa_batch_device")
+
+
+def gjkepa_batch_warm_device(version: int, tol_ff: float, vert_dtype: int, precision: int, verts_ptr: int,
+                             hull_off_ptr: int, hull_cnt_ptr: int, pairs_ptr: int, n_pairs: int, out_ptr: int,
+                             ws_ptr: int, ws_bytes: int, warm_ptr: int, stream: int = 0) -> None:
+    """gjkepa_batch_device with a per-pair warm-start slot array (device uint32[4 * n_pairs], in/out;
+    0xFFFFFFFF = none): persistent pairs whose last simplex still encloses the origin skip GJK, and
+    pairs that missed last time first try the hull-centre separating axis."""
+    rc = load().gjkepa_batch_warm_device(int(version), float(tol_ff), int(vert_dtype), int(precision), verts_ptr,
+                                         hull_off_ptr, hull_cnt_ptr, pairs_ptr, int(n_pairs), out_ptr, ws_ptr,
+                                         int(ws_bytes), warm_ptr, stream or None)
+    _check(rc, "gjkepa_batch_warm_device")
 
 
 def version_string() -> str:
