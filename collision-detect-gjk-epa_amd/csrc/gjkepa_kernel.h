@@ -135,6 +135,9 @@
 #ifndef GJKEPA_C1_MINW
 #define GJKEPA_C1_MINW 1
 #endif
+#ifndef GJKEPA_LDS_HULL_MIN
+#define GJKEPA_LDS_HULL_MIN 512     // tiers with G*K >= this read hull vertices from LDS, not registers
+#endif
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 5
 #define GJKEPA_CONTACT_TIERS 2

@@ -113,8 +113,19 @@ template <typename T, typename TH, int G, int K, int VC, int FC> struct Ctx {
     using L_t = Lds<T, TH, G, K, VC, FC>;
     L_t& L;
     Grp<G> g;
-    T ax[K], ay[K], az[K], bx[K], by[K], bz[K];
+    // Hull vertex k*G + gl of each hull: in registers, or (large-hull tiers, G*K >= GJKEPA_LDS_HULL_MIN)
+    // read from the group's LDS copy at each use, which frees 6K registers per lane so those
+    // tiers fit two waves per SIMD.  Same values either way (LDS holds the storage precision).
+    static constexpr bool kRegHull = G * K < GJKEPA_LDS_HULL_MIN;
+    T ax[kRegHull ? K : 1], ay[kRegHull ? K : 1], az[kRegHull ? K : 1];
+    T bx[kRegHull ? K : 1], by[kRegHull ? K : 1], bz[kRegHull ? K : 1];
     int na, nb;
+    DEV T Ax(int k) const { if constexpr (kRegHull) return ax[k]; else return (T)L.hx[0][k * G + g.gl]; }
+    DEV T Ay(int k) const { if constexpr (kRegHull) return ay[k]; else return (T)L.hy[0][k * G + g.gl]; }
+    DEV T Az(int k) const { if constexpr (kRegHull) return az[k]; else return (T)L.hz[0][k * G + g.gl]; }
+    DEV T Bx(int k) const { if constexpr (kRegHull) return bx[k]; else return (T)L.hx[1][k * G + g.gl]; }
+    DEV T By(int k) const { if constexpr (kRegHull) return by[k]; else return (T)L.hy[1][k * G + g.gl]; }
+    DEV T Bz(int k) const { if constexpr (kRegHull) return bz[k]; else return (T)L.hz[1][k * G + g.gl]; }
     DEV V3<T> A(int i) const { return vmk<T>((T)L.hx[0][i], (T)L.hy[0][i], (T)L.hz[0][i]); }
     DEV V3<T> B(int i) const { return vmk<T>((T)L.hx[1][i], (T)L.hy[1][i], (T)L.hz[1][i]); }
     DEV V3<T> vert(int i) const { return vmk<T>(L.u.e.vx[i], L.u.e.vy[i], L.u.e.vz[i]); }
@@ -132,8 +143,8 @@ CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
-        ta[k] = i < c.na ? d.x * c.ax[k] + d.y * c.ay[k] + d.z * c.az[k] : -Tol<T>::BIG;
-        tb[k] = i < c.nb ? -(d.x * c.bx[k] + d.y * c.by[k] + d.z * c.bz[k]) : -Tol<T>::BIG;
+        ta[k] = i < c.na ? d.x * c.Ax(k) + d.y * c.Ay(k) + d.z * c.Az(k) : -Tol<T>::BIG;
+        tb[k] = i < c.nb ? -(d.x * c.Bx(k) + d.y * c.By(k) + d.z * c.Bz(k)) : -Tol<T>::BIG;
         va = ta[k] > va ? ta[k] : va;
         vb = tb[k] > vb ? tb[k] : vb;
     }
@@ -743,7 +754,7 @@ CTX_T DEV T hull_dot_max(CTX& c, int side, V3<T> n) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         int i = k * G + c.g.gl;
-        T t = side ? n.x * c.bx[k] + n.y * c.by[k] + n.z * c.bz[k] : n.x * c.ax[k] + n.y * c.ay[k] + n.z * c.az[k];
+        T t = side ? n.x * c.Bx(k) + n.y * c.By(k) + n.z * c.Bz(k) : n.x * c.Ax(k) + n.y * c.Ay(k) + n.z * c.Az(k);
         if (i < (side ? c.nb : c.na) && t > mx) mx = t;
     }
     return gmax<G>(mx);
@@ -755,7 +766,7 @@ CTX_T DEV int hull_band_set(CTX& c, int side, V3<T> n, T mx, T band, bool store)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         int i = k * G + c.g.gl;
-        T px = side ? c.bx[k] : c.ax[k], py = side ? c.by[k] : c.ay[k], pz = side ? c.bz[k] : c.az[k];
+        T px = side ? c.Bx(k) : c.Ax(k), py = side ? c.By(k) : c.Ay(k), pz = side ? c.Bz(k) : c.Az(k);
         T t = n.x * px + n.y * py + n.z * pz;
         bool in = i < (side ? c.nb : c.na) && t > mx - band;
         uint64_t m = c.g.ballot(in);
@@ -1147,10 +1158,10 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             int i = k * G + gl;
-            const V3<T> da = vsub(vmk<T>(c.ax[k], c.ay[k], c.az[k]), m1);
+            const V3<T> da = vsub(vmk<T>(c.Ax(k), c.Ay(k), c.Az(k)), m1);
             const T ta = da.x * da.x + da.y * da.y + da.z * da.z;
             if (i < c.na && ta > r1) r1 = ta;
-            const V3<T> db = vsub(vmk<T>(c.bx[k], c.by[k], c.bz[k]), m2);
+            const V3<T> db = vsub(vmk<T>(c.Bx(k), c.By(k), c.Bz(k)), m2);
             const T tb = db.x * db.x + db.y * db.y + db.z * db.z;
             if (i < c.nb && tb > r2) r2 = tb;
         }
@@ -1164,8 +1175,8 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int i = k * G + gl;
-                const T ta = d.x * c.ax[k] + d.y * c.ay[k] + d.z * c.az[k];
-                const T tb = d.x * c.bx[k] + d.y * c.by[k] + d.z * c.bz[k];
+                const T ta = d.x * c.Ax(k) + d.y * c.Ay(k) + d.z * c.Az(k);
+                const T tb = d.x * c.Bx(k) + d.y * c.By(k) + d.z * c.Bz(k);
                 if (i < c.na && ta > amax) amax = ta;
                 if (i < c.nb && tb < bmin) bmin = tb;
             }
@@ -1307,8 +1318,10 @@ CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restric
         if (i < c.nb) { bx = pb[i]; by = pb[c.nb + i]; bz = pb[2 * c.nb + i]; }
         nonfinite = nonfinite || !isfinite(ax) || !isfinite(ay) || !isfinite(az) || !isfinite(bx) ||
                     !isfinite(by) || !isfinite(bz);
-        c.ax[k] = (T)ax; c.ay[k] = (T)ay; c.az[k] = (T)az;
-        c.bx[k] = (T)bx; c.by[k] = (T)by; c.bz[k] = (T)bz;
+        if constexpr (CTX::kRegHull) {
+            c.ax[k] = (T)ax; c.ay[k] = (T)ay; c.az[k] = (T)az;
+            c.bx[k] = (T)bx; c.by[k] = (T)by; c.bz[k] = (T)bz;
+        }
         c.L.hx[0][i] = ax; c.L.hy[0][i] = ay; c.L.hz[0][i] = az;
         c.L.hx[1][i] = bx; c.L.hy[1][i] = by; c.L.hz[1][i] = bz;
     }
@@ -1484,7 +1497,8 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
 // GJK kernel: sphere pre-test + GJK.  Misses and errors get their final record here; hits park the
 // simplex codes (5 words) in their own record slot and are routed to the smallest EPA tier that
 // holds their hulls.  Tier 0 takes every pair; hulls above its capacity are routed to tier 1.
-template <typename TIn, typename T, int G, int K, int MINW>
+// WARM instantiations serve gjkepa_batch_warm_device (a.warm set); the plain ones carry no warm code.
+template <typename TIn, typename T, int G, int K, int MINW, bool WARM>
 __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) {
     static_assert(G >= 4, "the tetrahedron faces run on quads");
     using L_t = Lds<T, TIn, G, K, 0, 0>;
@@ -1507,7 +1521,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         uint8_t next = 0;
         if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
             store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
-            if (a.warm && gl < 4) a.warm[4 * pair + gl] = kStale;
+            if (WARM && gl < 4) a.warm[4 * pair + gl] = kStale;
         } else if (na > K * G || nb > K * G) {
             next = GJKEPA_ROUTE_GJK1;                        // larger GJK tier
         } else {
@@ -1517,13 +1531,13 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
             GK_STAMP(SG_LOAD);
             if (bad_in) {
                 store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
-                if (a.warm && gl < 4) a.warm[4 * pair + gl] = kStale;
+                if (WARM && gl < 4) a.warm[4 * pair + gl] = kStale;
             } else {
                 uint32_t kc[4];
                 int gjk_it = 0;
                 int r = PH_MISS;
                 bool warm_hit = false, try_axis = false;
-                if (a.warm) {
+                if constexpr (WARM) {
                     try_axis = a.warm[4 * pair] == kWarmMiss;
                     if (!try_axis) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
                 }
@@ -1531,7 +1545,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                 else r = gjk_phase(c, kc, gjk_it, try_axis);
                 __builtin_amdgcn_wave_barrier();
                 GK_STAMP(SG_CHK);
-                if (a.warm && gl < 4)   // this call's simplex seeds the next call; a miss mark; none for errors
+                if (WARM && gl < 4)     // this call's simplex seeds the next call; a miss mark; none for errors
                     a.warm[4 * pair + gl] = r == PH_HIT ? (gl == 0 ? kc[0] : gl == 1 ? kc[1] : gl == 2 ? kc[2] : kc[3])
                                           : (r == PH_MISS && gl == 0) ? kWarmMiss : kStale;
                 if (r == PH_HIT) {
@@ -1815,7 +1829,7 @@ template <typename K_t> int grid_for(K_t kfn, size_t lds, int num_cus, int grid)
 
 template <typename TIn, typename T, int G, int K, int MINW>
 hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
-    auto kfn = gk::gjk_kernel<TIn, T, G, K, MINW>;
+    auto kfn = a.warm ? gk::gjk_kernel<TIn, T, G, K, MINW, true> : gk::gjk_kernel<TIn, T, G, K, MINW, false>;
     constexpr int GPW = 64 / G;
     const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 0, 0>) * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
