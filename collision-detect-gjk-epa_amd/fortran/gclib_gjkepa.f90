@@ -8,6 +8,9 @@
 !                 `!$OMP PARALLEL DO ... CALL GJKEPA` loop with one GPU submission.
 !   GJKEPA_LAST_STATUS  per-thread status of the last GJKEPA call (the reference PAUSEs/STOPs
 !                 instead, :300-301, :337-339, :1370-1372; here the call returns and reports).
+!   GJKEPA_BROADPHASE  the pairs (a < b) of a pooled hull set that pass the reference's own first
+!                 test, RoughCollisionDetection_SphericalEnvelope (:76-77, :1165-1188), computed on
+!                 the GPU: the list a caller's all-pairs GJKEPA loop reduces to.
 !
 ! Only ISO_C_BINDING is used (no hipfort).  Hulls are REAL*8 p(n,3) exactly like the reference.
 !---------------------------------------------------------------------------------------------
@@ -15,7 +18,7 @@ MODULE GCLIB_GJKEPA
     USE, INTRINSIC :: ISO_C_BINDING
     IMPLICIT NONE
     PRIVATE
-    PUBLIC :: GJKEPA, GJKEPA_BATCH, GJKEPA_LAST_STATUS, GJKEPA_SET_DEVICE
+    PUBLIC :: GJKEPA, GJKEPA_BATCH, GJKEPA_LAST_STATUS, GJKEPA_SET_DEVICE, GJKEPA_BROADPHASE
     PUBLIC :: GJKEPA_STATUS_OK, GJKEPA_STATUS_EPA_MAXITER, GJKEPA_STATUS_DEGENERATE
     PUBLIC :: GJKEPA_STATUS_BAD_VERSION, GJKEPA_STATUS_BAD_INPUT
 
@@ -64,6 +67,19 @@ MODULE GCLIB_GJKEPA
             TYPE(contact_f64), INTENT(OUT) :: out(*)
             INTEGER(C_INT) :: c_gjkepa_batch
         END FUNCTION c_gjkepa_batch
+
+        FUNCTION c_gjkepa_broadphase(vert_dtype, verts, n_vert_scalars, hull_off, hull_cnt, n_hulls, &
+                                     pairs, max_pairs, n_pairs, dev) BIND(C, NAME="gjkepa_broadphase")
+            IMPORT :: C_INT32_T, C_INT64_T, C_DOUBLE, C_INT
+            INTEGER(C_INT32_T), VALUE :: vert_dtype, dev
+            REAL(C_DOUBLE), INTENT(IN) :: verts(*)
+            INTEGER(C_INT64_T), VALUE :: n_vert_scalars, n_hulls, max_pairs
+            INTEGER(C_INT64_T), INTENT(IN) :: hull_off(*)
+            INTEGER(C_INT32_T), INTENT(IN) :: hull_cnt(*)
+            INTEGER(C_INT32_T), INTENT(OUT) :: pairs(*)
+            INTEGER(C_INT64_T), INTENT(OUT) :: n_pairs
+            INTEGER(C_INT) :: c_gjkepa_broadphase
+        END FUNCTION c_gjkepa_broadphase
 
         FUNCTION c_gjkepa_last_error() BIND(C, NAME="gjkepa_last_error")
             IMPORT :: C_PTR
@@ -167,6 +183,45 @@ CONTAINS
             status_(k) = rec(k)%status
         END DO
     END SUBROUTINE GJKEPA_BATCH
+
+    !-----------------------------------------------------------------------------------------
+    ! GJKEPA_BROADPHASE — candidate pairs of a pooled hull set (same pool layout as GJKEPA_BATCH).
+    !   pairs_(2, n)  ALLOCATABLE out: 1-based hull indices (a < b), ascending (a, b), exactly the
+    !                 pairs whose GJKEPA call would pass RoughCollisionDetection_SphericalEnvelope
+    !   info_         0, or a negative GJKEPA_E_* code (pairs_ then has size 0)
+    !-----------------------------------------------------------------------------------------
+    SUBROUTINE GJKEPA_BROADPHASE(verts_, hull_off_, hull_cnt_, pairs_, info_)
+        REAL*8,    INTENT(IN)  :: verts_(:)
+        INTEGER*8, INTENT(IN)  :: hull_off_(:)
+        INTEGER*4, INTENT(IN)  :: hull_cnt_(:)
+        INTEGER*4, ALLOCATABLE, INTENT(OUT) :: pairs_(:,:)
+        INTEGER*4, INTENT(OUT) :: info_
+        INTEGER(C_INT64_T), ALLOCATABLE :: off(:)
+        INTEGER(C_INT32_T), ALLOCATABLE :: buf(:)
+        INTEGER(C_INT64_T) :: nh, cap, nfound
+        INTEGER(C_INT) :: rc
+        nh = SIZE(hull_cnt_)
+        ALLOCATE(off(nh))
+        off = hull_off_ - 1
+        cap = MAX(8_C_INT64_T * nh, 1024_C_INT64_T)
+        DO
+            ALLOCATE(buf(2 * cap))
+            rc = c_gjkepa_broadphase(1_C_INT32_T, verts_, INT(SIZE(verts_), C_INT64_T), off, hull_cnt_, nh, &
+                                     buf, cap, nfound, device)
+            IF (rc /= 0 .OR. nfound <= cap) EXIT
+            cap = nfound                     ! the list was cut: call again with room for all of it
+            DEALLOCATE(buf)
+        END DO
+        IF (rc /= 0) THEN
+            CALL report(rc, "GJKEPA_BROADPHASE")
+            ALLOCATE(pairs_(2, 0))
+            info_ = rc
+            RETURN
+        END IF
+        ALLOCATE(pairs_(2, nfound))
+        pairs_ = RESHAPE(buf(1:2 * nfound), [2, INT(nfound)]) + 1
+        info_ = 0
+    END SUBROUTINE GJKEPA_BROADPHASE
 
     INTEGER*4 FUNCTION GJKEPA_LAST_STATUS()
         GJKEPA_LAST_STATUS = last_status

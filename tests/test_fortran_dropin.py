@@ -78,3 +78,32 @@ def test_fortran_quickhull_matches_oracle(orc, tmp_path):
         assert (st, nfb, nvb) == (r["status"][c], r["n_faces"][c], r["n_verts"][c])
         tri = np.array([int(x) for x in b[c][5:]]).reshape(-1, 3) - 1
         np.testing.assert_array_equal(tri, r["faces"][fo:fo + nfb])
+
+
+BP_EXE = os.path.join(ROOT, "tests", "fortran", "build", "test_broadphase")
+
+
+def test_broadphase_driver_built():
+    assert os.path.exists(BP_EXE), "run __graft_entry__.build()"
+
+
+@pytest.mark.gpu
+def test_fortran_broadphase_matches_oracle(orc, tmp_path):
+    """USE GCLIB_GJKEPA; CALL GJKEPA_BROADPHASE(...): the reference sphere test's pair list for a
+    pooled hull set, 1-based and ascending, identical to the oracle's."""
+    import gjkepa
+    pool = gjkepa.synth_scene(77, 400, 8, 40, 12.0, dtype=np.float64)
+    path = tmp_path / "hulls.txt"
+    with open(path, "w") as fh:
+        fh.write(f"{pool.hull_cnt.size}\n")
+        for h in range(pool.hull_cnt.size):
+            p = pool.hull(h)
+            fh.write(f"{len(p)}\n" + "".join(f"{x:.17g} {y:.17g} {z:.17g}\n" for x, y, z in p))
+    out = subprocess.run([BP_EXE, str(path)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    n, info = (int(x) for x in lines[0].split()[1:])
+    got = np.array([[int(x) for x in ln.split()[1:]] for ln in lines[1:] if ln.startswith("P")]).reshape(-1, 2) - 1
+    want, m = orc.broadphase(pool.verts, pool.hull_off, pool.hull_cnt)
+    assert info == 0 and n == m > 0
+    np.testing.assert_array_equal(got, want)
