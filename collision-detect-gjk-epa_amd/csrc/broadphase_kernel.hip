@@ -13,9 +13,10 @@
 //                     cells); 63-bit cell keys (iz, iy, ix), coordinates wrapped at 2^21.
 //   3. radix sort of (cell key, hull) pairs (rocPRIM via hipCUB); gather of the spheres into cell
 //      order, so neighbouring threads read neighbouring entries.
-//   4. grid_kernel<count>: thread p binary-searches the 9 cell rows (ix-1..ix+1 is one key range)
-//      around its cell and tests the hulls there with a larger index; exclusive scan of the counts;
-//      grid_kernel<emit> writes (a << 32 | b) keys at the offsets.
+//   4. cell_table_kernel: hash table (cell key -> first sorted position) from the segment starts;
+//      grid_kernel<count>: thread p walks the 9 cell rows around its cell (ix-1..ix+1 is one key
+//      range: first non-empty cell by table lookup, then forward) and tests the hulls there with a
+//      larger index; exclusive scan of the counts; grid_kernel<emit> writes (a << 32 | b) keys.
 //   5. radix sort of the max_pairs keys (padded with all-ones); unpack to int32 (a, b) pairs.
 // Memory-latency-bound integer / fp64 work (binary searches, short candidate runs), no MFMA.
 #include <hip/hip_runtime.h>
@@ -45,7 +46,8 @@ DEV_BP uint64_t cell_key(uint64_t ix, uint64_t iy, uint64_t iz) { return ((iz & 
 // the centre is bit-exact), then every lane takes vertices gl, gl+SG, ... for the radius (a max,
 // order-free).  One thread per hull instead would issue 64 scattered loads per instruction.
 constexpr int SG = 16;
-constexpr int SPHERE_BLOCK = 128;   // 8 hulls per block: 24 KB (fp32) / 48 KB (fp64) of LDS staging
+constexpr int SPHERE_BLOCK = 128;   // 8 hulls per block
+constexpr int SPHERE_STAGE = 64;    // hulls of up to 64 vertices are staged: 6 KB (fp32) of LDS per block
 template <typename TIn>
 __global__ __launch_bounds__(SPHERE_BLOCK) void sphere_kernel(const TIn* __restrict__ verts, const int64_t* __restrict__ hull_off,
                                                               const int32_t* __restrict__ hull_cnt, int64_t n_hulls,
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(SPHERE_BLOCK) void sphere_kernel(const TIn* __restr
                                                               double* __restrict__ cz, double* __restrict__ cr,
                                                               unsigned long long* __restrict__ rmax_bits) {
     constexpr int GPB = SPHERE_BLOCK / SG;
-    __shared__ TIn stage[GPB][3 * GJKEPA_MAX_HULL_VERTS];
+    __shared__ TIn stage[GPB][3 * SPHERE_STAGE];
     __shared__ double cen[GPB][3];
     __shared__ unsigned long long blk;
     const int gl = threadIdx.x % SG, grp = threadIdx.x / SG;
@@ -64,15 +66,23 @@ __global__ __launch_bounds__(SPHERE_BLOCK) void sphere_kernel(const TIn* __restr
         const int64_t h = base + grp;
         const int n = h < n_hulls ? hull_cnt[h] : 0;
         const bool in = h < n_hulls && n >= 1 && n <= GJKEPA_MAX_HULL_VERTS;
-        if (in) {
-            const TIn* p = verts + hull_off[h];
+        const TIn* p = in ? verts + hull_off[h] : verts;
+        if (in && n <= SPHERE_STAGE)
             for (int i = gl; i < 3 * n; i += SG) stage[grp][i] = p[i];
-        }
         __syncthreads();
-        const TIn* q = stage[grp];
+        const TIn* q = n <= SPHERE_STAGE ? stage[grp] : p;   // larger hulls are read in place
         if (in && gl < 3) {   // SUM(p(:,k)) / SIZE(p,1), sequential in index order (:1175-1176)
+            const TIn* col = q + gl * n;
             double sum = 0.0;
-            for (int i = 0; i < n; ++i) sum += (double)q[gl * n + i];
+            int i = 0;
+            for (; i + 8 <= n; i += 8) {   // loads batched ahead of the in-order adds
+                TIn v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = col[i + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) sum += (double)v[u];
+            }
+            for (; i < n; ++i) sum += (double)col[i];
             cen[grp][gl] = sum / (double)n;
         }
         __syncthreads();
@@ -137,24 +147,46 @@ __global__ __launch_bounds__(256) void gather_kernel(int64_t n, const int32_t* _
     }
 }
 
-DEV_BP int64_t lower_bound(const uint64_t* __restrict__ keys, int64_t n, uint64_t k) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t md = (lo + hi) >> 1;
-        if (keys[md] < k) lo = md + 1; else hi = md;
-    }
-    return lo;
+// Cell table: open-addressing hash (linear probing) from a cell key to the first sorted position
+// of that cell, built from the segment starts of the sorted keys; a lookup costs ~1 probe instead of
+// a 20-step binary search over the whole key array.
+DEV_BP uint64_t mix64(uint64_t x) {
+    x ^= x >> 31; x *= 0x7FB5D329728EA185ull; x ^= x >> 27; x *= 0x81DADEF4BC2DD44Dull; x ^= x >> 33;
+    return x;
 }
 
-// the hulls q of sorted positions with cell keys in [kl, kh] that form a passing pair with hull a
+__global__ __launch_bounds__(256) void cell_table_kernel(int64_t n, const uint64_t* __restrict__ keys,
+                                                         unsigned long long* __restrict__ tkeys,
+                                                         int32_t* __restrict__ tstart, uint64_t tmask) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[p];
+        if (k == kInvalid || (p > 0 && keys[p - 1] == k)) continue;
+        for (uint64_t h = mix64(k) & tmask;; h = (h + 1) & tmask) {
+            const unsigned long long prev = atomicCAS(&tkeys[h], (unsigned long long)kInvalid, (unsigned long long)k);
+            if (prev == (unsigned long long)kInvalid) { tstart[h] = (int32_t)p; break; }
+        }
+    }
+}
+
+// first sorted position of cell k, -1 when the cell is empty
+DEV_BP int64_t cell_start(const unsigned long long* __restrict__ tkeys, const int32_t* __restrict__ tstart,
+                          uint64_t tmask, uint64_t k) {
+    for (uint64_t h = mix64(k) & tmask;; h = (h + 1) & tmask) {
+        const uint64_t t = tkeys[h];
+        if (t == k) return tstart[h];
+        if (t == kInvalid) return -1;
+    }
+}
+
+// the hulls q from sorted position q0 on while their cell key is <= kh that form a passing pair with hull a
 // (larger index); returns how many, writing their keys from out[o] on when EMIT
 template <bool EMIT>
-DEV_BP int64_t visit_range(uint64_t kl, uint64_t kh, int64_t n, const uint64_t* __restrict__ keys,
+DEV_BP int64_t visit_range(int64_t q0, uint64_t kh, int64_t n, const uint64_t* __restrict__ keys,
                            const double* __restrict__ sx, const double* __restrict__ sy, const double* __restrict__ sz,
                            const double* __restrict__ sr, const int32_t* __restrict__ order, int32_t a, double x,
                            double y, double z, double r, uint64_t* __restrict__ out, int64_t o, int64_t max_pairs) {
     int64_t c = 0;
-    for (int64_t q = lower_bound(keys, n, kl); q < n && keys[q] <= kh; ++q) {
+    for (int64_t q = q0; q < n && keys[q] <= kh; ++q) {
         const int32_t b = order[q];
         if (b <= a) continue;
         // NORM2(mp1 - mp2) <= r1 + r2 + TOL (:1185), mp1 = hull a
@@ -174,9 +206,11 @@ template <bool EMIT>
 __global__ __launch_bounds__(256) void grid_kernel(int64_t n, const uint64_t* __restrict__ keys,
                                                    const double* __restrict__ sx, const double* __restrict__ sy,
                                                    const double* __restrict__ sz, const double* __restrict__ sr,
-                                                   const int32_t* __restrict__ order, int64_t* __restrict__ counts,
-                                                   const int64_t* __restrict__ offs, uint64_t* __restrict__ out,
-                                                   int64_t max_pairs) {
+                                                   const int32_t* __restrict__ order,
+                                                   const unsigned long long* __restrict__ tkeys,
+                                                   const int32_t* __restrict__ tstart, uint64_t tmask,
+                                                   int64_t* __restrict__ counts, const int64_t* __restrict__ offs,
+                                                   uint64_t* __restrict__ out, int64_t max_pairs) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = keys[p];
         int64_t c = 0;
@@ -188,14 +222,19 @@ __global__ __launch_bounds__(256) void grid_kernel(int64_t n, const uint64_t* __
             const bool row = ix >= 1 && ix + 1 <= kMask;          // ix-1..ix+1 contiguous in key order
             for (int t = 0; t < 9; ++t) {
                 const uint64_t jy = iy + (uint64_t)(t % 3) - 1, jz = iz + (uint64_t)(t / 3) - 1;
-                if (row) {
-                    c += visit_range<EMIT>(cell_key(ix - 1, jy, jz), cell_key(ix + 1, jy, jz), n, keys, sx, sy, sz, sr,
-                                           order, a, x, y, z, r, out, o + c, max_pairs);
-                } else {   // the row wraps at 2^21: its three cells separately
+                if (row) {   // the row's first non-empty cell, then forward through the row
+                    int64_t q0 = -1;
+                    for (uint64_t jx = ix - 1; jx != ix + 2 && q0 < 0; ++jx) q0 = cell_start(tkeys, tstart, tmask, cell_key(jx, jy, jz));
+                    if (q0 >= 0)
+                        c += visit_range<EMIT>(q0, cell_key(ix + 1, jy, jz), n, keys, sx, sy, sz, sr, order, a, x, y, z,
+                                               r, out, o + c, max_pairs);
+                } else {     // the row wraps at 2^21: its three cells separately
                     for (uint64_t jx = ix - 1; jx != ix + 2; ++jx) {
                         const uint64_t kc = cell_key(jx, jy, jz);
-                        c += visit_range<EMIT>(kc, kc, n, keys, sx, sy, sz, sr, order, a, x, y, z, r, out, o + c,
-                                               max_pairs);
+                        const int64_t q0 = cell_start(tkeys, tstart, tmask, kc);
+                        if (q0 >= 0)
+                            c += visit_range<EMIT>(q0, kc, n, keys, sx, sy, sz, sr, order, a, x, y, z, r, out, o + c,
+                                                   max_pairs);
                     }
                 }
             }
@@ -227,7 +266,9 @@ constexpr size_t kAlign = 256;
 size_t up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
-    size_t cx, cy, cz, cr, rmax, cell, keys0, idx, skeys, order, sx, sy, sz, sr, counts, offs, pk, pk2, temp, total;
+    size_t cx, cy, cz, cr, rmax, cell, keys0, idx, skeys, order, sx, sy, sz, sr, counts, offs, tkeys, tstart, pk, pk2,
+        temp, total;
+    uint64_t tsize;
     size_t sort1, scan, sort2;
 };
 
@@ -251,6 +292,9 @@ Layout layout(int64_t n, int64_t max_pairs, size_t sort1, size_t scan, size_t so
     L.keys0 = take(d); L.idx = take(i); L.skeys = take(d); L.order = take(i);
     L.sx = take(d); L.sy = take(d); L.sz = take(d); L.sr = take(d);
     L.counts = take((size_t)(n + 1) * 8); L.offs = take((size_t)(n + 1) * 8);
+    L.tsize = 1024;
+    while (L.tsize < 2 * (uint64_t)n) L.tsize *= 2;           // load factor <= 1/2
+    L.tkeys = take(L.tsize * 8); L.tstart = take(L.tsize * 4);
     L.pk = take((size_t)max_pairs * 8); L.pk2 = take((size_t)max_pairs * 8);
     L.sort1 = sort1; L.scan = scan; L.sort2 = sort2;
     L.temp = take(std::max(sort1, std::max(scan, sort2)));
@@ -306,9 +350,14 @@ hipError_t gjkepa_enqueue_broadphase(int vert_dtype, const void* verts, const in
                        at<double>(ws, L.cy), at<double>(ws, L.cz), at<double>(ws, L.cr), at<double>(ws, L.sx),
                        at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr));
     if ((e = hipMemsetAsync(at<int64_t>(ws, L.counts) + n, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(at<void>(ws, L.tkeys), 0xFF, L.tsize * 8, s)) != hipSuccess) return e;
+    const uint64_t tmask = L.tsize - 1;
+    hipLaunchKernelGGL(cell_table_kernel, dim3(nb), dim3(256), 0, s, n, (const uint64_t*)at<uint64_t>(ws, L.skeys),
+                       at<unsigned long long>(ws, L.tkeys), at<int32_t>(ws, L.tstart), tmask);
     hipLaunchKernelGGL(grid_kernel<false>, dim3(nb), dim3(256), 0, s, n, at<uint64_t>(ws, L.skeys), at<double>(ws, L.sx),
                        at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr), at<int32_t>(ws, L.order),
-                       at<int64_t>(ws, L.counts), (const int64_t*)nullptr, (uint64_t*)nullptr, max_pairs);
+                       (const unsigned long long*)at<unsigned long long>(ws, L.tkeys), (const int32_t*)at<int32_t>(ws, L.tstart),
+                       tmask, at<int64_t>(ws, L.counts), (const int64_t*)nullptr, (uint64_t*)nullptr, max_pairs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     tb = L.scan;
     if ((e = hipcub::DeviceScan::ExclusiveSum(at<void>(ws, L.temp), tb, at<int64_t>(ws, L.counts),
@@ -319,7 +368,9 @@ hipError_t gjkepa_enqueue_broadphase(int vert_dtype, const void* verts, const in
         if ((e = hipMemsetAsync(at<uint64_t>(ws, L.pk), 0xFF, (size_t)max_pairs * 8, s)) != hipSuccess) return e;
         hipLaunchKernelGGL(grid_kernel<true>, dim3(nb), dim3(256), 0, s, n, at<uint64_t>(ws, L.skeys), at<double>(ws, L.sx),
                            at<double>(ws, L.sy), at<double>(ws, L.sz), at<double>(ws, L.sr), at<int32_t>(ws, L.order),
-                           (int64_t*)nullptr, at<int64_t>(ws, L.offs), at<uint64_t>(ws, L.pk), max_pairs);
+                           (const unsigned long long*)at<unsigned long long>(ws, L.tkeys),
+                           (const int32_t*)at<int32_t>(ws, L.tstart), tmask, (int64_t*)nullptr, at<int64_t>(ws, L.offs),
+                           at<uint64_t>(ws, L.pk), max_pairs);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tb = L.sort2;
         if ((e = hipcub::DeviceRadixSort::SortKeys(at<void>(ws, L.temp), tb, at<uint64_t>(ws, L.pk),
