@@ -120,14 +120,11 @@ def main():
     out = torch.zeros(n * rec_bytes, dtype=torch.uint8, device=dev)
     ws_bytes = gjkepa.workspace_bytes(n)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
-    gathered = None
-    # RCCL path: two record buffers; step i's all-gather (RCCL's own stream) overlaps step i+1's
-    # kernels, and a buffer is rewritten only after the gather that read it has finished
-    overlap = world > 1 and not args.no_gather and not host_coll and not args.no_overlap
-    outs = [out, torch.zeros_like(out)] if overlap else [out]
+    # N > 1: every step's records are all-gathered (shard.RecordExchange); on RCCL step i's gather
+    # overlaps step i+1's kernels (two record buffers), on gloo it is staged through host memory
+    ex = None
     if world > 1 and not args.no_gather:
-        gathered = [torch.empty(world * n * rec_bytes, dtype=torch.uint8, device=dev) for _ in outs]
-    works = [None] * len(outs)
+        ex = shard.RecordExchange(n * rec_bytes, world, dev, overlap=not args.no_overlap, host_staged=host_coll)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -136,34 +133,20 @@ def main():
                                    cnt.data_ptr(), prs.data_ptr(), n, o.data_ptr(), ws.data_ptr(), ws_bytes, sptr)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    nstep = [0]
 
     def step(i=None):
-        b = nstep[0] % len(outs)
-        nstep[0] += 1
-        if works[b] is not None:
-            works[b].wait()             # the compute stream waits for the gather that read outs[b]
-            works[b] = None
+        o = ex.buffer() if ex else out       # a reused buffer first waits for the gather that read it
         if i is not None:
             ev[i][0].record(stream)
-        launch(prec, outs[b])
+        launch(prec, o)
         if i is not None:
             ev[i][1].record(stream)
-        if gathered is not None:
-            if host_coll:
-                g = torch.empty(world * n * rec_bytes, dtype=torch.uint8)
-                dist.all_gather_into_tensor(g, outs[b].cpu())
-                gathered[b].copy_(g)
-            elif overlap:
-                works[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
-            else:
-                dist.all_gather_into_tensor(gathered[b], outs[b])
+        if ex:
+            ex.submit()
 
     def drain():
-        for k, w in enumerate(works):
-            if w is not None:
-                w.wait()
-                works[k] = None
+        if ex:
+            ex.drain()
 
     for _ in range(args.warmup):
         step()
@@ -191,7 +174,7 @@ def main():
     value = total_pairs * args.steps / elapsed / 1e6
 
     # statistics of the last step's records (rank-local)
-    recs = np.frombuffer(outs[(nstep[0] - 1) % len(outs)].cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
+    recs = np.frombuffer((ex.last if ex else out).cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
     hit_rate = float((recs["collision"] != 0).mean())
     status_counts = {int(k): int(v) for k, v in zip(*np.unique(recs["status"], return_counts=True))}
     epa_iters = (recs["diag"] >> 8) & 0xFF
@@ -229,7 +212,7 @@ def main():
                                f"version_={args.version}, TOL_FF_=1.0, hull B offset r~U[0,{rmax}]",
                    "hull_vertices": [nmin, nmax],
                    "pairs_per_gpu": n, "total_pairs": total_pairs, "seed": SEED,
-                   "parallelism": f"shard{world}" + ("" if gathered is None else "+allgather_overlapped" if overlap
+                   "parallelism": f"shard{world}" + ("" if ex is None else "+allgather_overlapped" if ex.overlap
                                                        else "+allgather"),
                    "vert_storage": "f32", "record_bytes": rec_bytes},
         "roofline": roofline,

@@ -198,14 +198,15 @@ int gjkepa_hull_batch_device(int32_t vert_dtype, const void* points,
  * RoughCollisionDetection_SphericalEnvelope (GCLIB_GJKEPA.f90:1165-1188):
  *   m = SUM(p(:,k)) / n (sequential sums), r = MAXVAL(NORM2(p_i - m)),
  *   pair iff NORM2(m_a - m_b) <= r_a + r_b + 1.0      (fp64, the oracle's arithmetic, bit-exact)
- * i.e. exactly the pairs whose GJKEPA call would get past its first test (:76-80); a caller's
+ * i.e. exactly the pairs whose GJKEPA call would get past its first test (:76-77); a caller's
  * double loop over all pairs collapses to this list.  Hulls with a bad vertex count or non-finite
  * coordinates take part in no pair.
  *
- * Method (MI355X): per-hull sphere kernel; radix sort of the spheres' x-extent lower bounds
- * (rocPRIM); sweep kernels (count, exclusive scan, emit) test each sphere against the ones after
- * it in x order until the extents separate; a final radix sort of the emitted (a << 32 | b) keys
- * leaves the list in ascending (a, b) order — the order of `DO a = 1, N; DO b = a+1, N`.
+ * Method (MI355X): per-hull sphere kernel; uniform grid of cell edge 2 r_max + 1 with a radix
+ * sort of the cell keys (rocPRIM) and a hash table from cell to first sorted hull; count / scan /
+ * emit kernels test each hull against the later-indexed hulls of its 27 neighbouring cells; a final
+ * radix sort of the emitted (a << 32 | b) keys leaves the list in ascending (a, b) order — the
+ * order of `DO a = 1, N; DO b = a+1, N`.
  * Output: pairs[2k], pairs[2k+1] = (a, b) for k < min(n_found, max_pairs); *n_pairs = n_found
  * (device int64 for the device entry).  n_found > max_pairs means the list was cut: enlarge it and
  * call again.  The device entry never synchronises (graph-capturable): the final sort runs over

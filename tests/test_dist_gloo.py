@@ -51,3 +51,36 @@ def test_sharded_allgather_matches_single_process(tmp_path, orc):
     whole = gjkepa.synth_pairs(0x6A4B5C1D, TOTAL, 32, 32, 2.5)
     ref = orc.gjkepa_batch(whole, 2, 1.0)
     assert gathered.tobytes() == ref.view(np.uint8).reshape(-1).tobytes()
+
+
+def _exchange_worker(rank, world, port, outdir, overlap, host_staged):
+    sys.path[:0] = [os.path.join(ROOT, "collision-detect-gjk-epa_amd")]
+    import torch.distributed as dist
+
+    import shard
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ex = shard.RecordExchange(1000, world, "cpu", overlap=overlap, host_staged=host_staged)
+    for step in range(7):                    # what bench.py does per step: fill a buffer, submit it
+        buf = ex.buffer()
+        buf.fill_(16 * rank + step)
+        ex.submit()
+    ex.drain()
+    if rank == 0:
+        np.save(os.path.join(outdir, f"last_{overlap}_{host_staged}.npy"), ex.last_gathered.numpy())
+        np.save(os.path.join(outdir, f"nbuf_{overlap}_{host_staged}.npy"), np.array([len(ex.local)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_record_exchange_overlapped_and_inline(tmp_path):
+    """shard.RecordExchange, the per-step all-gather bench.py runs for N > 1: the rotating-buffer
+    overlapped mode (RCCL on MI355X, gloo here), the in-line mode and the host-staged mode all end
+    with every rank's last-step records, in rank order."""
+    world = 2
+    for overlap, staged in [(True, False), (False, False), (False, True)]:
+        mp.spawn(_exchange_worker, args=(world, _free_port(), str(tmp_path), overlap, staged), nprocs=world, join=True)
+        last = np.load(tmp_path / f"last_{overlap}_{staged}.npy")
+        want = np.concatenate([np.full(1000, 16 * r + 6, np.uint8) for r in range(world)])
+        assert np.array_equal(last, want), (overlap, staged)
+        assert int(np.load(tmp_path / f"nbuf_{overlap}_{staged}.npy")[0]) == (2 if overlap and not staged else 1)
