@@ -44,10 +44,10 @@ DEV void lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <int G, int K> struct HullLds {
+template <typename TP, int G, int K> struct HullLds {
     static constexpr int NP = G * K;
     static constexpr int FC = 2 * NP - 4;
-    double px[NP], py[NP], pz[NP];
+    TP px[NP], py[NP], pz[NP];          // points at storage precision (widened exactly on use)
     double fnx[FC], fny[FC], fnz[FC];   // unit normals (UNINML of the stored order)
     uint32_t fv[FC];                    // packed vertex ids; DEAD = removed slot with no successor
     uint32_t hl[FC];                    // horizon edges u | w << 10, in (visible face, edge) order
@@ -56,8 +56,8 @@ template <int G, int K> struct HullLds {
     uint8_t used[NP];                   // point referenced by a live face (output pass)
 };
 
-template <int G, int K> struct Cloud {
-    using L_t = HullLds<G, K>;
+template <typename TP, int G, int K> struct Cloud {
+    using L_t = HullLds<TP, G, K>;
     static constexpr int FC = L_t::FC;
     static constexpr int R = (FC + G - 1) / G;
     L_t& L;
@@ -66,7 +66,7 @@ template <int G, int K> struct Cloud {
     int st[K];                          // assigned face slot, -1 = interior / processed / absent
     double ds[K];                       // distance above the assigned face
     int n;
-    DEV V3<double> P(int i) const { return vmk<double>(L.px[i], L.py[i], L.pz[i]); }
+    DEV V3<double> P(int i) const { return vmk<double>((double)L.px[i], (double)L.py[i], (double)L.pz[i]); }
     DEV V3<double> mine(int k) const { return vmk<double>(x[k], y[k], z[k]); }
     DEV double fdist(int f, V3<double> p) const {   // qh_dist: dot(p - p_a, n_f)
         const V3<double> a = P(id0(L.fv[f]));
@@ -77,7 +77,7 @@ template <int G, int K> struct Cloud {
 // group-wide (value, index) argmax over the lane's own points; `val(k, i)` gives point i's value,
 // or -DBL_MAX when it does not take part.  First index wins ties (lower k first within a lane,
 // since index k*G+gl grows with k; lowest index across lanes).
-template <int G, int K, typename F> DEV void point_argmax(const Cloud<G, K>& c, F val, double& v, int& idx) {
+template <typename TP, int G, int K, typename F> DEV void point_argmax(const Cloud<TP, G, K>& c, F val, double& v, int& idx) {
     v = -DBL_MAX;
     idx = 0x7fffffff;
 #pragma unroll
@@ -91,8 +91,8 @@ template <int G, int K, typename F> DEV void point_argmax(const Cloud<G, K>& c, 
 }
 
 // the cloud's hull; returns a GJKEPA_STATUS_* code.  On OK, hwm is the face high-water mark.
-template <int G, int K> DEV int build(Cloud<G, K>& c, int& hwm_out) {
-    using C = Cloud<G, K>;
+template <typename TP, int G, int K> DEV int build(Cloud<TP, G, K>& c, int& hwm_out) {
+    using C = Cloud<TP, G, K>;
     auto& L = c.L;
     const int gl = c.g.gl, n = c.n, fcap = 2 * n - 4;
     const double eps = GJKEPA_HULL_EPS;
@@ -238,7 +238,7 @@ template <int G, int K> DEV int build(Cloud<G, K>& c, int& hwm_out) {
             for (int k = 0; k < K; ++k) { best[k] = -DBL_MAX; bk[k] = 0; }
             for (int kk = 0; kk < nh; ++kk) {
                 const int s = kk < nvis ? (int)L.vl[kk] : hwm + (kk - nvis);
-                const V3<double> a = c.P(id0(L.fv[s]));
+                const V3<double> a = c.P((int)(L.hl[kk] & 1023u));   // new face kk = (u, w, eye)
                 const V3<double> nn = vmk<double>(L.fnx[s], L.fny[s], L.fnz[s]);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -262,7 +262,7 @@ template <int G, int K> DEV int build(Cloud<G, K>& c, int& hwm_out) {
     return GJKEPA_STATUS_OK;
 }
 
-template <typename TIn, int G, int K> DEV void run_cloud(Cloud<G, K>& c, const gjkepa_hull_args& a, int64_t ci) {
+template <typename TIn, int G, int K> DEV void run_cloud(Cloud<TIn, G, K>& c, const gjkepa_hull_args& a, int64_t ci) {
     auto& L = c.L;
     const int gl = c.g.gl;
     const int n = a.cloud_cnt[ci];
@@ -278,7 +278,7 @@ template <typename TIn, int G, int K> DEV void run_cloud(Cloud<G, K>& c, const g
             if (i < n) {
                 c.x[k] = (double)src[i]; c.y[k] = (double)src[n + i]; c.z[k] = (double)src[2 * n + i];
                 finite &= isfinite(c.x[k]) && isfinite(c.y[k]) && isfinite(c.z[k]);
-                L.px[i] = c.x[k]; L.py[i] = c.y[k]; L.pz[i] = c.z[k];
+                L.px[i] = src[i]; L.py[i] = src[n + i]; L.pz[i] = src[2 * n + i];
             } else {
                 c.x[k] = c.y[k] = c.z[k] = 0.0;
             }
@@ -340,8 +340,8 @@ __global__ __launch_bounds__(64, 1) void hull_kernel(const gjkepa_hull_args a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
     const int grp = lane / G;
-    HullLds<G, K>* Ls = reinterpret_cast<HullLds<G, K>*>(smem);
-    Cloud<G, K> c{Ls[grp]};
+    HullLds<TIn, G, K>* Ls = reinterpret_cast<HullLds<TIn, G, K>*>(smem);
+    Cloud<TIn, G, K> c{Ls[grp]};
     const bool tier0 = a.tier == 0;
     for (int64_t chunk = blockIdx.x; chunk * 64 < a.n_clouds; chunk += gridDim.x) {
         const int64_t ci = chunk * 64 + lane;
@@ -370,7 +370,7 @@ namespace {
 template <typename TIn, int G, int K> hipError_t launch_tier(gjkepa_hull_args a, int lo, hipStream_t s) {
     auto kfn = gk::qh::hull_kernel<TIn, G, K>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::qh::HullLds<G, K>) * GPW;
+    const size_t lds = sizeof(gk::qh::HullLds<TIn, G, K>) * GPW;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     const int64_t chunks = (a.n_clouds + 63) / 64;
