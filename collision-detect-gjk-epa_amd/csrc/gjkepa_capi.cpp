@@ -62,6 +62,7 @@ struct DeviceState {
     DevBuf verts, off, cnt, pairs, out, ws;
     DevBuf h_foff, h_faces, h_nf, h_nv, h_st, h_hv, h_vi;   // gjkepa_hull_batch staging
     DevBuf b_pairs, b_count, b_ws;                          // gjkepa_broadphase staging
+    DevBuf c_idx, c_hits, c_ws, c_n;                        // gjkepa_collide staging
 };
 
 std::mutex g_table_mu;
@@ -503,6 +504,97 @@ int gjkepa_compact_hits_device(int32_t precision, const void* records, int64_t n
                                                   : (int)offsetof(gjkepa_contact_f32, collision);
     e = gjkepa_enqueue_compact(records, n_pairs, rb, flag, hit_idx, hits, n_hits, workspace, s);
     return e == hipSuccess ? 0 : hip_fail(e, "compaction launch");
+}
+
+// ---- whole collision step: broad phase -> narrow phase -> hit list (host buffers) ---------------
+int gjkepa_collide(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
+                   int64_t n_vert_scalars, const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
+                   int32_t* pairs, void* out, int64_t max_contacts, int64_t* n_contacts, int64_t* n_candidates,
+                   int32_t device) {
+    if (n_hulls < 0 || max_contacts < 0 || n_vert_scalars < 0 || n_hulls > INT32_MAX - 1 || !valid_enums(vert_dtype, precision))
+        return fail(GJKEPA_E_ARG, "bad sizes/dtype/precision");
+    if (!n_contacts || (max_contacts > 0 && (!pairs || !out))) return fail(GJKEPA_E_ARG, "null pointer");
+    *n_contacts = 0;
+    if (n_candidates) *n_candidates = 0;
+    if (n_hulls == 0) return 0;
+    if (!verts || !hull_off || !hull_cnt) return fail(GJKEPA_E_ARG, "null pointer");
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        const int64_t c = hull_cnt[h];
+        if (c >= 1 && c <= GJKEPA_MAX_HULL_VERTS && (hull_off[h] < 0 || hull_off[h] + 3 * c > n_vert_scalars))
+            return fail(GJKEPA_E_ARG, "hull outside the vertex pool");
+    }
+    int rc = 0;
+    DeviceState* d = device_state(device, &rc);
+    if (!d) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    if ((rc = init_device(d, device))) return rc;
+    const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
+    const size_t rec = (size_t)gjkepa_record_bytes(precision);
+    hipStream_t s = d->stream;
+    hipError_t e;
+    if ((e = d->verts.ensure((size_t)n_vert_scalars * esz)) != hipSuccess || (e = d->off.ensure((size_t)n_hulls * 8)) != hipSuccess ||
+        (e = d->cnt.ensure((size_t)n_hulls * 4)) != hipSuccess || (e = d->b_count.ensure(8)) != hipSuccess ||
+        (e = d->c_n.ensure(8)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    if ((e = hipMemcpyAsync(d->verts.p, verts, (size_t)n_vert_scalars * esz, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->off.p, hull_off, (size_t)n_hulls * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d->cnt.p, hull_cnt, (size_t)n_hulls * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    // broad phase: a list of 8 candidates per hull first; one more pass at the exact size if it was cut
+    int64_t cap = n_hulls * 8 > 1024 ? n_hulls * 8 : 1024, ncand = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (cap > INT32_MAX) return fail(GJKEPA_E_ARG, "candidate list above 2^31-1 pairs");
+        const int64_t wsb = gjkepa_broadphase_ws_bytes(n_hulls, cap);
+        if (wsb < 0) return fail(GJKEPA_E_HIP, "broad phase workspace query failed");
+        if ((e = d->b_pairs.ensure((size_t)cap * 8 + 8)) != hipSuccess || (e = d->b_ws.ensure((size_t)wsb)) != hipSuccess)
+            return hip_fail(e, "hipMalloc");
+        rc = gjkepa_broadphase_device(vert_dtype, d->verts.p, (const int64_t*)d->off.p, (const int32_t*)d->cnt.p,
+                                      n_hulls, (int32_t*)d->b_pairs.p, cap, (int64_t*)d->b_count.p, d->b_ws.p,
+                                      (int64_t)d->b_ws.cap, s);
+        if (rc) return rc;
+        if ((e = hipMemcpyAsync(&ncand, d->b_count.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync D2H");
+        if (ncand <= cap) break;
+        cap = ncand;
+    }
+    if (n_candidates) *n_candidates = ncand;
+    if (ncand == 0) return 0;
+    // narrow phase on the device-resident list, then the dense hit list
+    const int64_t wsn = gjkepa_workspace_bytes(ncand), wsc = gjkepa_compact_ws_bytes(ncand);
+    if (wsc < 0) return fail(GJKEPA_E_HIP, "compaction workspace query failed");
+    if ((e = d->out.ensure((size_t)ncand * rec)) != hipSuccess || (e = d->ws.ensure((size_t)wsn)) != hipSuccess ||
+        (e = d->c_idx.ensure((size_t)ncand * 4)) != hipSuccess || (e = d->c_hits.ensure((size_t)ncand * rec)) != hipSuccess ||
+        (e = d->c_ws.ensure((size_t)wsc)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    if ((rc = enqueue(version, tol_ff, vert_dtype, precision, d->verts.p, (const int64_t*)d->off.p,
+                      (const int32_t*)d->cnt.p, (const int32_t*)d->b_pairs.p, ncand, d->out.p, d->ws.p,
+                      (int64_t)d->ws.cap, s, d->num_cus)))
+        return rc;
+    const int flag = precision == GJKEPA_PREC_F64 ? (int)offsetof(gjkepa_contact_f64, collision)
+                                                  : (int)offsetof(gjkepa_contact_f32, collision);
+    if ((e = gjkepa_enqueue_compact(d->out.p, ncand, (int)rec, flag, (int32_t*)d->c_idx.p, d->c_hits.p,
+                                    (int64_t*)d->c_n.p, d->c_ws.p, s)) != hipSuccess)
+        return hip_fail(e, "compaction launch");
+    int64_t nh = 0;
+    if ((e = hipMemcpyAsync(&nh, d->c_n.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    *n_contacts = nh;
+    const int64_t m = nh < max_contacts ? nh : max_contacts;
+    if (m > 0) {
+        std::vector<int32_t> idx((size_t)m), cand((size_t)ncand * 2);
+        if ((e = hipMemcpyAsync(idx.data(), d->c_idx.p, (size_t)m * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipMemcpyAsync(cand.data(), d->b_pairs.p, (size_t)ncand * 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipMemcpyAsync(out, d->c_hits.p, (size_t)m * rec, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync D2H");
+        for (int64_t k = 0; k < m; ++k) {
+            pairs[2 * k] = cand[2 * (size_t)idx[k]];
+            pairs[2 * k + 1] = cand[2 * (size_t)idx[k] + 1];
+        }
+    }
+    return 0;
 }
 
 }  // extern "C"

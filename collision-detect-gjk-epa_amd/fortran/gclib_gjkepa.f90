@@ -11,6 +11,8 @@
 !   GJKEPA_BROADPHASE  the pairs (a < b) of a pooled hull set that pass the reference's own first
 !                 test, RoughCollisionDetection_SphericalEnvelope (:76-77, :1165-1188), computed on
 !                 the GPU: the list a caller's all-pairs GJKEPA loop reduces to.
+!   GJKEPA_COLLIDE  the whole all-pairs loop in one call: broad phase, GJKEPA on every candidate,
+!                 and only the colliding pairs returned with their GJKEPA outputs.
 !
 ! Only ISO_C_BINDING is used (no hipfort).  Hulls are REAL*8 p(n,3) exactly like the reference.
 !---------------------------------------------------------------------------------------------
@@ -18,7 +20,7 @@ MODULE GCLIB_GJKEPA
     USE, INTRINSIC :: ISO_C_BINDING
     IMPLICIT NONE
     PRIVATE
-    PUBLIC :: GJKEPA, GJKEPA_BATCH, GJKEPA_LAST_STATUS, GJKEPA_SET_DEVICE, GJKEPA_BROADPHASE
+    PUBLIC :: GJKEPA, GJKEPA_BATCH, GJKEPA_LAST_STATUS, GJKEPA_SET_DEVICE, GJKEPA_BROADPHASE, GJKEPA_COLLIDE
     PUBLIC :: GJKEPA_STATUS_OK, GJKEPA_STATUS_EPA_MAXITER, GJKEPA_STATUS_DEGENERATE
     PUBLIC :: GJKEPA_STATUS_BAD_VERSION, GJKEPA_STATUS_BAD_INPUT
 
@@ -80,6 +82,22 @@ MODULE GCLIB_GJKEPA
             INTEGER(C_INT64_T), INTENT(OUT) :: n_pairs
             INTEGER(C_INT) :: c_gjkepa_broadphase
         END FUNCTION c_gjkepa_broadphase
+
+        FUNCTION c_gjkepa_collide(version, tol_ff, vert_dtype, precision, verts, n_vert_scalars, &
+                                  hull_off, hull_cnt, n_hulls, pairs, out, max_contacts, n_contacts, &
+                                  n_candidates, dev) BIND(C, NAME="gjkepa_collide")
+            IMPORT :: C_INT32_T, C_INT64_T, C_DOUBLE, C_INT, contact_f64
+            INTEGER(C_INT32_T), VALUE :: version, vert_dtype, precision, dev
+            REAL(C_DOUBLE), VALUE     :: tol_ff
+            REAL(C_DOUBLE), INTENT(IN) :: verts(*)
+            INTEGER(C_INT64_T), VALUE :: n_vert_scalars, n_hulls, max_contacts
+            INTEGER(C_INT64_T), INTENT(IN) :: hull_off(*)
+            INTEGER(C_INT32_T), INTENT(IN) :: hull_cnt(*)
+            INTEGER(C_INT32_T), INTENT(OUT) :: pairs(*)
+            TYPE(contact_f64), INTENT(OUT) :: out(*)
+            INTEGER(C_INT64_T), INTENT(OUT) :: n_contacts, n_candidates
+            INTEGER(C_INT) :: c_gjkepa_collide
+        END FUNCTION c_gjkepa_collide
 
         FUNCTION c_gjkepa_last_error() BIND(C, NAME="gjkepa_last_error")
             IMPORT :: C_PTR
@@ -222,6 +240,65 @@ CONTAINS
         pairs_ = RESHAPE(buf(1:2 * nfound), [2, INT(nfound)]) + 1
         info_ = 0
     END SUBROUTINE GJKEPA_BROADPHASE
+
+    !-----------------------------------------------------------------------------------------
+    ! GJKEPA_COLLIDE — every colliding pair of a pooled hull set (same pool layout as GJKEPA_BATCH),
+    ! i.e. the caller's `DO a; DO b = a+1; CALL GJKEPA(...); IF (collision_) ...` loop in one call.
+    !   pairs_(2, n)           ALLOCATABLE out: 1-based (a < b), ascending, only pairs with collision_
+    !   outputs (…, n)          ALLOCATABLE out: GJKEPA's INTENT(OUT) values for those pairs
+    !   info_                  0, or a negative GJKEPA_E_* code (everything then has size 0)
+    !-----------------------------------------------------------------------------------------
+    SUBROUTINE GJKEPA_COLLIDE(version_, TOL_FF_, verts_, hull_off_, hull_cnt_, pairs_, colliType_, &
+                              nearest_points_, collision_normal_, collision_point_, penetration_depth_, &
+                              status_, info_)
+        INTEGER*4, INTENT(IN)  :: version_
+        REAL*8,    INTENT(IN)  :: TOL_FF_
+        REAL*8,    INTENT(IN)  :: verts_(:)
+        INTEGER*8, INTENT(IN)  :: hull_off_(:)
+        INTEGER*4, INTENT(IN)  :: hull_cnt_(:)
+        INTEGER*4, ALLOCATABLE, INTENT(OUT) :: pairs_(:,:), colliType_(:), status_(:)
+        REAL*8,    ALLOCATABLE, INTENT(OUT) :: nearest_points_(:,:,:), collision_normal_(:,:)
+        REAL*8,    ALLOCATABLE, INTENT(OUT) :: collision_point_(:,:), penetration_depth_(:)
+        INTEGER*4, INTENT(OUT) :: info_
+        TYPE(contact_f64), ALLOCATABLE :: rec(:)
+        INTEGER(C_INT64_T), ALLOCATABLE :: off(:)
+        INTEGER(C_INT32_T), ALLOCATABLE :: buf(:)
+        INTEGER(C_INT64_T) :: nh, cap, nhit, ncand
+        INTEGER(C_INT) :: rc
+        INTEGER :: k, n
+        nh = SIZE(hull_cnt_)
+        ALLOCATE(off(nh))
+        off = hull_off_ - 1
+        cap = MAX(4_C_INT64_T * nh, 1024_C_INT64_T)
+        DO
+            ALLOCATE(buf(2 * cap), rec(cap))
+            rc = c_gjkepa_collide(INT(version_, C_INT32_T), TOL_FF_, 1_C_INT32_T, 1_C_INT32_T, verts_, &
+                                  INT(SIZE(verts_), C_INT64_T), off, hull_cnt_, nh, buf, rec, cap, nhit, &
+                                  ncand, device)
+            IF (rc /= 0 .OR. nhit <= cap) EXIT
+            cap = nhit                       ! more hits than room: call again with room for all
+            DEALLOCATE(buf, rec)
+        END DO
+        n = 0
+        IF (rc == 0) n = INT(nhit)
+        ALLOCATE(pairs_(2, n), colliType_(n), status_(n), nearest_points_(2, 3, n), collision_normal_(3, n), &
+                 collision_point_(3, n), penetration_depth_(n))
+        info_ = rc
+        IF (rc /= 0) THEN
+            CALL report(rc, "GJKEPA_COLLIDE")
+            RETURN
+        END IF
+        DO k = 1, n
+            pairs_(:, k) = buf(2 * k - 1 : 2 * k) + 1
+            colliType_(k) = rec(k)%colli_type
+            nearest_points_(1, :, k) = rec(k)%nearest_points(1:3)
+            nearest_points_(2, :, k) = rec(k)%nearest_points(4:6)
+            collision_normal_(:, k) = rec(k)%collision_normal
+            collision_point_(:, k) = rec(k)%collision_point
+            penetration_depth_(k) = rec(k)%penetration_depth
+            status_(k) = rec(k)%status
+        END DO
+    END SUBROUTINE GJKEPA_COLLIDE
 
     INTEGER*4 FUNCTION GJKEPA_LAST_STATUS()
         GJKEPA_LAST_STATUS = last_status

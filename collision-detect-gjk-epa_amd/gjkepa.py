@@ -33,6 +33,7 @@ EXPORTS = (
     "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
     "gjkepa_broadphase_workspace_bytes", "gjkepa_broadphase", "gjkepa_broadphase_device", "gjkepa_synth_scene",
     "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
+    "gjkepa_collide",
 )
 HULL_MAX_POINTS = 256
 
@@ -116,6 +117,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_batch_warm_device.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                              c_vp, c_vp]
     lib.gjkepa_batch_warm_device.restype = ctypes.c_int
+    lib.gjkepa_collide.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                   c_vp, c_i32]
+    lib.gjkepa_collide.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -435,3 +439,28 @@ def compact_hits_device(precision: int, records_ptr: int, n_pairs: int, hit_idx_
     rc = load().gjkepa_compact_hits_device(int(precision), records_ptr, int(n_pairs), hit_idx_ptr, hits_ptr or None,
                                            n_hits_ptr, ws_ptr, int(ws_bytes), stream or None)
     _check(rc, "gjkepa_compact_hits_device")
+
+
+def collide(pool: HullPool, version: int = 2, tol_ff: float = 1.0, precision: int = PREC_F64,
+            max_contacts: int | None = None, device: int = 0):
+    """The all-pairs GJKEPA loop over a hull pool in one call (broad phase, narrow phase, hit list).
+    Returns (pairs int32 [n, 2] with a < b ascending, records of those hits, n_candidates)."""
+    lib = load()
+    verts = np.ascontiguousarray(pool.verts)
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    cap = max_contacts if max_contacts is not None else max(4 * cnt.size, 1024)
+    while True:
+        prs = np.zeros((max(cap, 1), 2), np.int32)
+        out = np.zeros(max(cap, 1), dtype=record_dtype(precision))
+        nc = np.zeros(1, np.int64)
+        ncand = np.zeros(1, np.int64)
+        rc = lib.gjkepa_collide(int(version), float(tol_ff), pool.dtype_code, int(precision), _ptr(verts), verts.size,
+                                _ptr(off), _ptr(cnt), cnt.size, _ptr(prs), _ptr(out), cap, _ptr(nc), _ptr(ncand),
+                                int(device))
+        _check(rc, "gjkepa_collide")
+        n = int(nc[0])
+        if n <= cap or max_contacts is not None:
+            m = min(n, cap)
+            return prs[:m], out[:m], int(ncand[0])
+        cap = n

@@ -254,6 +254,18 @@ int gjkepa_batch_warm_device(int32_t version, double tol_ff, int32_t vert_dtype,
                              void* out, void* workspace, int64_t workspace_bytes,
                              uint32_t* warm, void* stream);
 
+/* ---- whole collision step (host buffers, blocking) ---------------------------------------------
+ * The reference caller's `DO a; DO b = a+1; CALL GJKEPA(...)` over a pooled hull set in one call:
+ * gjkepa_broadphase_device -> gjkepa_batch_device on the candidate list -> gjkepa_compact_hits_device.
+ * Writes the first min(n, max_contacts) hits: pairs[2k], pairs[2k+1] = (a, b) (a < b, ascending)
+ * and out[k] = that pair's record (gjkepa_contact_f64 / _f32 by precision), bit-exact with GJKEPA
+ * on (p_a, p_b).  *n_contacts = hits found; *n_candidates (may be NULL) = pairs past the sphere test. */
+int gjkepa_collide(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                   const void* verts, int64_t n_vert_scalars,
+                   const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
+                   int32_t* pairs, void* out, int64_t max_contacts,
+                   int64_t* n_contacts, int64_t* n_candidates, int32_t device);
+
 /* Last error message of the calling thread ("" if none). */
 const char* gjkepa_last_error(void);
 

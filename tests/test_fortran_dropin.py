@@ -107,3 +107,44 @@ def test_fortran_broadphase_matches_oracle(orc, tmp_path):
     want, m = orc.broadphase(pool.verts, pool.hull_off, pool.hull_cnt)
     assert info == 0 and n == m > 0
     np.testing.assert_array_equal(got, want)
+
+
+CL_EXE = os.path.join(ROOT, "tests", "fortran", "build", "test_collide")
+
+
+def test_collide_driver_built():
+    assert os.path.exists(CL_EXE), "run __graft_entry__.build()"
+
+
+@pytest.mark.gpu
+def test_fortran_collide_matches_oracle(orc, tmp_path):
+    """USE GCLIB_GJKEPA; CALL GJKEPA_COLLIDE(...): the caller's all-pairs GJKEPA loop in one call —
+    the colliding pairs (1-based, ascending) with GJKEPA's outputs, equal to the oracle's broad
+    phase + GJKEPA on each candidate (reals printed with 17 significant digits: exact)."""
+    import gjkepa
+    pool = gjkepa.synth_scene(78, 300, 8, 40, 10.0, dtype=np.float64)
+    path = tmp_path / "hulls.txt"
+    with open(path, "w") as fh:
+        fh.write(f"{pool.hull_cnt.size}\n")
+        for h in range(pool.hull_cnt.size):
+            p = pool.hull(h)
+            fh.write(f"{len(p)}\n" + "".join(f"{x:.17g} {y:.17g} {z:.17g}\n" for x, y, z in p))
+    out = subprocess.run([CL_EXE, str(path)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    n, info = (int(x) for x in lines[0].split()[1:])
+    rows = [ln.split()[1:] for ln in lines[1:] if ln.startswith("C")]
+    cand, _ = orc.broadphase(pool.verts, pool.hull_off, pool.hull_cnt)
+    cand = cand.reshape(-1, 2)
+    sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, np.ascontiguousarray(cand.reshape(-1)))
+    recs = orc.gjkepa_batch(sub, 2, 1.0)
+    hit = recs["collision"] != 0
+    assert info == 0 and n == int(hit.sum()) == len(rows) > 0
+    got_pairs = np.array([[int(r[0]), int(r[1])] for r in rows]) - 1
+    np.testing.assert_array_equal(got_pairs, cand[hit])
+    want = recs[hit]
+    for r, w in zip(rows, want):
+        assert int(r[2]) == w["colli_type"] and int(r[3]) == w["status"]
+        vals = np.array([float(x) for x in r[4:]])
+        ref = np.concatenate([[w["penetration_depth"]], w["collision_normal"], w["collision_point"]])
+        np.testing.assert_array_equal(vals, ref)
