@@ -135,6 +135,9 @@
 #ifndef GJKEPA_C1_MINW
 #define GJKEPA_C1_MINW 1
 #endif
+#ifndef GJKEPA_AXIS_REJECT
+#define GJKEPA_AXIS_REJECT 1        // cold GJK first tries the centre axis as a separating axis
+#endif
 #ifndef GJKEPA_LDS_HULL_MIN
 #define GJKEPA_LDS_HULL_MIN 512     // tiers with G*K >= this read hull vertices from LDS, not registers
 #endif

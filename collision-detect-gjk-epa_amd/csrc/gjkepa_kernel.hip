@@ -1169,7 +1169,11 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
         r2 = tsqrt(gmax<G>(r2));
         GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
-        if (try_axis) {   // warm start, pair missed last call: the centre axis separates the hulls
+        // Quick reject: the axis between the hull centres separates the hulls by more than
+        // kWarmMargin, so the origin is that far outside the Minkowski difference and GJK can only
+        // end in the reference's miss (all-zero record, diag 0).  Cold calls try it on every pair;
+        // warm calls on pairs that missed last call.
+        if (try_axis) {
             const V3<T> d = vsub(m2, m1);
             T amax = -Tol<T>::BIG, bmin = Tol<T>::BIG;
 #pragma unroll
@@ -1182,7 +1186,8 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
             }
             amax = gmax<G>(amax);
             bmin = gmin<G>(bmin);
-            if (c.g.unib(bmin - amax > T(kWarmMargin) * norm2(d))) return PH_MISS;
+            const T margin = sizeof(T) == 8 ? T(kWarmMargin) : T(1e-4);
+            if (c.g.unib(bmin - amax > margin * norm2(d))) return PH_MISS;
         }
     }
     // --- initial simplex (:82-170)
@@ -1536,10 +1541,11 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                 uint32_t kc[4];
                 int gjk_it = 0;
                 int r = PH_MISS;
-                bool warm_hit = false, try_axis = false;
+                bool warm_hit = false, try_axis = GJKEPA_AXIS_REJECT != 0;
                 if constexpr (WARM) {
-                    try_axis = a.warm[4 * pair] == kWarmMiss;
-                    if (!try_axis) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
+                    const bool was_miss = a.warm[4 * pair] == kWarmMiss;
+                    try_axis = try_axis || was_miss;
+                    if (!was_miss) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
                 }
                 if (warm_hit) r = PH_HIT;
                 else r = gjk_phase(c, kc, gjk_it, try_axis);
