@@ -1170,9 +1170,10 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
         GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
         // Quick reject: the axis between the hull centres separates the hulls by more than
-        // kWarmMargin, so the origin is that far outside the Minkowski difference and GJK can only
-        // end in the reference's miss (all-zero record, diag 0).  Cold calls try it on every pair;
-        // warm calls on pairs that missed last call.
+        // kWarmMargin.  Warm calls try it on pairs that missed last call; cold calls only with
+        // GJKEPA_AXIS_REJECT, because the reference's GJK does not always end in a miss for such a
+        // pair: on separated tie-heavy hulls (corner-to-corner cubes) it reports a hit whose EPA
+        // then degenerates (tests/test_axis_reject.py).
         if (try_axis) {
             const V3<T> d = vsub(m2, m1);
             T amax = -Tol<T>::BIG, bmin = Tol<T>::BIG;
