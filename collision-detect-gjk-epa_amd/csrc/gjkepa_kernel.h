@@ -136,10 +136,8 @@
 #define GJKEPA_C1_MINW 1
 #endif
 #ifndef GJKEPA_AXIS_REJECT
-#define GJKEPA_AXIS_REJECT 0        // 1: cold GJK first tries the centre axis as a separating axis.
-                                    // Off: the reference's GJK reports hits (then DEGENERATE) for some
-                                    // separated tie-heavy pairs, which the reject would turn into misses
-                                    // (tests/test_axis_reject.py); parity comes first.
+#define GJKEPA_AXIS_REJECT 1        // cold GJK tries the centre axis as a separating axis after the
+                                    // initial-simplex block (tests/test_axis_reject.py)
 #endif
 #ifndef GJKEPA_LDS_HULL_MIN
 #define GJKEPA_LDS_HULL_MIN 512     // tiers with G*K >= this read hull vertices from LDS, not registers

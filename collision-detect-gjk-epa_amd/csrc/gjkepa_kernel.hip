@@ -1128,6 +1128,7 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
     auto& L = c.L;
     const int gl = c.g.gl;
     gjk_it = 0;
+    bool axis_sep = false;
     {   // RoughCollisionDetection_SphericalEnvelope (:1165-1188)
         // the six sequential coordinate sums run on group lanes (sum j on lane j % G: hull j/3, axis j%3)
 #pragma unroll
@@ -1170,10 +1171,9 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
         GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
         // Quick reject: the axis between the hull centres separates the hulls by more than
-        // kWarmMargin.  Warm calls try it on pairs that missed last call; cold calls only with
-        // GJKEPA_AXIS_REJECT, because the reference's GJK does not always end in a miss for such a
-        // pair: on separated tie-heavy hulls (corner-to-corner cubes) it reports a hit whose EPA
-        // then degenerates (tests/test_axis_reject.py).
+        // kWarmMargin; a pair the initial-simplex block does not call a hit is then a miss without
+        // the tetrahedron loop.  Warm calls try it on pairs that missed last call, cold calls when
+        // GJKEPA_AXIS_REJECT is set.
         if (try_axis) {
             const V3<T> d = vsub(m2, m1);
             T amax = -Tol<T>::BIG, bmin = Tol<T>::BIG;
@@ -1188,7 +1188,7 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
             amax = gmax<G>(amax);
             bmin = gmin<G>(bmin);
             const T margin = sizeof(T) == 8 ? T(kWarmMargin) : T(1e-4);
-            if (c.g.unib(bmin - amax > margin * norm2(d))) return PH_MISS;
+            axis_sep = c.g.unib(bmin - amax > margin * norm2(d));
         }
     }
     // --- initial simplex (:82-170)
@@ -1223,6 +1223,9 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
         if (c.g.unib(quad_inside(q, s0, s1, s2, s3, nq))) enter = true;
     }
     GK_STAMP(SG_INIT);
+    // the quick reject answers only after the initial-simplex block: that block is where the
+    // reference reports hits for separated tie-heavy hulls (origin on the initial triangle's plane)
+    if (!enter && axis_sep) return PH_MISS;
     if (!enter) {
         // cycle history (:193-194): coordinate j < 12 of last1 / last2 lives on group lane j % G,
         // slot j / G
