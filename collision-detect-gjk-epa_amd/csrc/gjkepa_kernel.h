@@ -136,8 +136,10 @@
 #define GJKEPA_C1_MINW 1
 #endif
 #ifndef GJKEPA_AXIS_REJECT
-#define GJKEPA_AXIS_REJECT 1        // cold GJK tries the centre axis as a separating axis after the
-                                    // initial-simplex block (tests/test_axis_reject.py)
+#define GJKEPA_AXIS_REJECT 0        // diagnostic A/B only, never the product build: GJK answers "miss"
+                                    // when the centre axis separates the hulls.  Not parity-safe: the
+                                    // reference's tetra loop reports hits on separated hulls through
+                                    // isPointInSimplex's on-face branch (:1246-1256)
 #endif
 #ifndef GJKEPA_LDS_HULL_MIN
 #define GJKEPA_LDS_HULL_MIN 512     // tiers with G*K >= this read hull vertices from LDS, not registers

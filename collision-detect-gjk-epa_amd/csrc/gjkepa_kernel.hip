@@ -1091,9 +1091,8 @@ CTX_T DEV void update_simplex_c(const CTX& c, V3<T> nq, V3<T>& s0, V3<T>& s1, V3
 // tetrahedron never qualifies), the pair is a hit and EPA starts from it: GJK's iterations are
 // skipped.  Otherwise the call runs the reference GJK from scratch.  Results then agree with a cold
 // call to EPA's tolerance rather than bit for bit (a different start polytope).
-// A pair that missed is marked kWarmMiss; its next call first tries the axis between the hull
-// centres (the sphere test's means) and answers a miss when it separates the hulls by more than
-// kWarmMargin — the reference's own output for a miss (all zero), without GJK's iterations.
+// A pair that missed is marked kWarmMiss; its next call runs the reference GJK (a shortcut for
+// misses is not parity-safe: the reference reports hits on some separated hulls).
 constexpr double kWarmMargin = 1e-6;
 constexpr uint32_t kWarmMiss = 0xFFFFFFFEu;
 CTX_T DEV bool warm_start(CTX& c, const uint32_t* w, uint32_t* kc) {
@@ -1170,10 +1169,11 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
         r2 = tsqrt(gmax<G>(r2));
         GK_STAMP(SG_SPHERE);
         if (!c.g.unib(norm2(vsub(m1, m2)) <= r1 + r2 + T(1))) return PH_MISS;
-        // Quick reject: the axis between the hull centres separates the hulls by more than
-        // kWarmMargin; a pair the initial-simplex block does not call a hit is then a miss without
-        // the tetrahedron loop.  Warm calls try it on pairs that missed last call, cold calls when
-        // GJKEPA_AXIS_REJECT is set.
+        // Diagnostic quick reject (GJKEPA_AXIS_REJECT builds only): the axis between the hull
+        // centres separates the hulls by more than kWarmMargin, so a pair the initial-simplex block
+        // does not call a hit is answered "miss" without the tetrahedron loop.  NOT parity-safe:
+        // the reference's loop can still report a hit on such a pair through isPointInSimplex's
+        // on-face branch (:1246-1256), e.g. a unit cube vs the cube moved by (-1, 0, 2).
         if (try_axis) {
             const V3<T> d = vsub(m2, m1);
             T amax = -Tol<T>::BIG, bmin = Tol<T>::BIG;
@@ -1545,14 +1545,12 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                 uint32_t kc[4];
                 int gjk_it = 0;
                 int r = PH_MISS;
-                bool warm_hit = false, try_axis = GJKEPA_AXIS_REJECT != 0;
-                if constexpr (WARM) {
-                    const bool was_miss = a.warm[4 * pair] == kWarmMiss;
-                    try_axis = try_axis || was_miss;
-                    if (!was_miss) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
+                bool warm_hit = false;
+                if constexpr (WARM) {    // a pair that missed last call runs the reference GJK again
+                    if (a.warm[4 * pair] != kWarmMiss) warm_hit = warm_start(c, a.warm + 4 * pair, kc);
                 }
                 if (warm_hit) r = PH_HIT;
-                else r = gjk_phase(c, kc, gjk_it, try_axis);
+                else r = gjk_phase(c, kc, gjk_it, GJKEPA_AXIS_REJECT != 0);
                 __builtin_amdgcn_wave_barrier();
                 GK_STAMP(SG_CHK);
                 if (WARM && gl < 4)     // this call's simplex seeds the next call; a miss mark; none for errors

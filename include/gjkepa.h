@@ -242,12 +242,11 @@ int gjkepa_compact_hits_device(int32_t precision, const void* records, int64_t n
  * 0xFFFFFFFF (fill the array with 0xFF bytes for a first call).  When that simplex, rebuilt from the
  * current vertices, holds the origin strictly inside (every face more than 1e-6 from it), the pair
  * is a hit and EPA starts from it, skipping GJK; otherwise the reference GJK runs.  A pair that
- * missed is marked 0xFFFFFFFE (first word): its next call first tests the axis between the two hull
- * centres and answers the reference's miss (all-zero record) when that axis separates the hulls by
- * more than 1e-6.  On exit every slot holds this call's simplex (hits), the miss mark, or
- * 0xFFFFFFFF (errors).  Pairs with no warm data are bit-exact with gjkepa_batch_device; warm-started
+ * missed is marked 0xFFFFFFFE (first word) and runs the reference GJK on its next call.  On exit
+ * every slot holds this call's simplex (hits), the miss mark, or 0xFFFFFFFF (errors).  Pairs that
+ * are not warm-started are bit-exact with gjkepa_batch_device (hit flags always are); warm-started
  * hits agree with a cold call within EPA's own tolerance (a different start polytope), not bit for
- * bit, and warm misses differ from a cold call only in the diag word. */
+ * bit. */
 int gjkepa_batch_warm_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
                              const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
                              const int32_t* pairs, int64_t n_pairs,

@@ -41,6 +41,11 @@
 #define SPHERE_TOL 1.0    /* :1172 */
 #define SUPPORT_BAND 1.0e-1 /* :471-472, :792 */
 
+/* Branch coverage (test infrastructure): the reference branches a pair took, as a bit mask per pair
+ * (ORC_BR_* in gjkepa_oracle.h), collected in a thread-local word while the pair runs. */
+static _Thread_local uint64_t g_cov;
+#define COV(b) (g_cov |= (1ull << (b)))
+
 #define OVCAP 1024
 #define OFCAP 2048
 
@@ -149,6 +154,7 @@ static int is_inside_pf(const v3* V, int nn, v3 P) {
     int anypos = 0;
     for (int i = 0; i < nn; ++i) if (cp[i] > TOL_POS) anypos = 1;
     if (!anypos) {
+        COV(ORC_BR_IPF_XZ);
         for (int i = 0; i < nn; ++i) {
             int j = (i == nn - 1) ? 0 : i + 1;
             cp[i] = (V[j].x - V[i].x) * (P.z - V[i].z) - (V[j].z - V[i].z) * (P.x - V[i].x);
@@ -167,7 +173,7 @@ static v3 centroid4(const v3* S) {   /* SUM(simplex_(:,k)) / 4.D0 (:1086, :1232)
               (((S[0].z + S[1].z) + S[2].z) + S[3].z) / 4.0);
 }
 
-/* isPointInSimplex (:1217-1265) */
+/* isPointInSimplex (:1217-1265): 0 outside, 1 strictly inside (:1260), 2 the on-face branch */
 static int is_point_in_simplex(v3 P, const v3* S) {
     v3 M = centroid4(S);
     v3 nml[4];
@@ -182,7 +188,7 @@ static int is_point_in_simplex(v3 P, const v3* S) {
     for (int i = 0; i < 4; ++i) {
         if (fabs(dist[i]) < TOL_PT) {
             v3 V[3] = {S[IDFC[i][0]], S[IDFC[i][1]], S[IDFC[i][2]]};
-            if (is_inside_pf(V, 3, P)) return 1;
+            if (is_inside_pf(V, 3, P)) return 2;             /* on-face branch (:1246-1256) */
         }
     }
     return dist[0] > 0.0 && dist[1] > 0.0 && dist[2] > 0.0 && dist[3] > 0.0;
@@ -313,6 +319,7 @@ static int hull_insert(hullbuf* H, v3 p) {
     int ch, st = hull_add(H, H->nv, &ch);
     if (st) return st;
     if (ch) H->nv++;
+    else COV(ORC_BR_EPA_SWALLOW);                   /* QuickHull swallowed the point (:1005) */
     return 0;
 }
 
@@ -331,7 +338,7 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
     for (;;) {
         ++iter;
         *iters = iter;
-        if (iter > EPA_MAXIT) return GJKEPA_STATUS_EPA_MAXITER;                   /* :299-302 */
+        if (iter > EPA_MAXIT) { COV(ORC_BR_EPA_CAP); return GJKEPA_STATUS_EPA_MAXITER; }   /* :299-302 */
         int F1, ml = 0, st;
         double minv;
         v3 dir, a1, M;
@@ -357,6 +364,7 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
         minv = H->d1[ml];
         double dt = dot(vsub(a1, ORIGIN), dir);
         if (fabs(dt) < TOL_Z) {                                                    /* :905-908 */
+            COV(ORC_BR_EPA_CENTROID);
             double sx = 0.0, sy = 0.0, sz = 0.0;
             for (int j = 0; j < 3; ++j)
                 for (int f = 0; f < F1; ++f) {
@@ -367,9 +375,10 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
             M = mk(sx / cnt, sy / cnt, sz / cnt);
             dt = dot(vsub(a1, M), dir);
         }
-        if (dt <= -TOL_Z) dir = vneg(dir);                                          /* :910 */
+        if (dt <= -TOL_Z) { dir = vneg(dir); COV(ORC_BR_EPA_FLIP); }                /* :910 */
         v3 sp = support(A, B, dir);                                                  /* :914 */
         int two = fabs(minv) < TOL_Z;                                                /* :935 */
+        if (two) COV(ORC_BR_EPA_TWO);
         /* --- hull of (polytope vertices + new point(s)) (:918-950) --- */
         if (iter == 1) {
             v3 P[6];
@@ -408,8 +417,10 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
             qsort(H->d2, (size_t)F2, sizeof(double), cmp_dbl);
             stop = 1;
             for (int f = 0; f < F1; ++f) if (!(fabs(H->d1[f] - H->d2[f]) < TOL_PT)) { stop = 0; break; }
+            if (stop) COV(ORC_BR_EPA_STOP_EQUAL);
         } else {
             stop = F1 > F2;
+            if (stop) COV(ORC_BR_EPA_STOP_SHRINK);
         }
         if (stop) { *depth = minv2; *normal = dir2; return 0; }
     }
@@ -459,10 +470,11 @@ static int contact_v1(const hull_t* a, const hull_t* b, v3 n, v3* res) {
     scan_top2(b, vneg(n), i2);
     if (i1[0] < 0 || i2[0] < 0) return GJKEPA_STATUS_DEGENERATE;   /* index 0: out of bounds */
     *res = ORIGIN;
-    if (i1[0] == i1[1] && i2[0] == i2[1]) *res = vdiv(vadd(hv(a, i1[0]), hv(b, i2[0])), 2.0);
-    if (i1[0] != i1[1] && i2[0] == i2[1]) *res = hv(b, i2[0]);
-    else if (i1[0] == i1[1] && i2[0] != i2[1]) *res = hv(a, i1[0]);
+    if (i1[0] == i1[1] && i2[0] == i2[1]) { *res = vdiv(vadd(hv(a, i1[0]), hv(b, i2[0])), 2.0); COV(ORC_BR_V1_MID); }
+    if (i1[0] != i1[1] && i2[0] == i2[1]) { *res = hv(b, i2[0]); COV(ORC_BR_V1_B); }
+    else if (i1[0] == i1[1] && i2[0] != i2[1]) { *res = hv(a, i1[0]); COV(ORC_BR_V1_A); }
     if (i1[0] != i1[1] && i2[0] != i2[1]) {
+        COV(ORC_BR_V1_MEAN);
         double mx = -DBL_MAX;
         for (int i = 0; i < a->n; ++i) { double t = dot(n, hv(a, i)); if (t > mx) mx = t; }
         double sx = 0.0, sy = 0.0, sz = 0.0;
@@ -488,6 +500,7 @@ static void foot_ll(v3 P1, v3 Q1, v3 P2, v3 Q2, v3* f1, v3* f2) {
     double a = dot(d1, d1), b = dot(d1, d2), c = dot(d1, r), e = dot(d2, d2), f = dot(d2, r);
     double d = a * e - b * b;
     if (fabs(d) < TOL_Z) {
+        COV(ORC_BR_FOOTLL_PARALLEL);
         *f1 = vdiv(vadd(P1, Q1), 2.0);
         *f2 = foot_pl(*f1, P2, Q2);
     } else {
@@ -513,7 +526,7 @@ static int overlap(const v3* p, int n) {
 /* SORT_CLOCK (:1513-1575): angular order about the centroid.  The reference leaves the result
  * undefined when all points coincide (returns before assigning); here the input is returned. */
 static int sort_clock(const v3* p, int n, v3* o) {
-    if (overlap(p, n)) { memcpy(o, p, sizeof(v3) * (size_t)n); return 0; }
+    if (overlap(p, n)) { COV(ORC_BR_V2_OVERLAP); memcpy(o, p, sizeof(v3) * (size_t)n); return 0; }
     double sx = 0.0, sy = 0.0, sz = 0.0;
     for (int i = 0; i < n; ++i) { sx += p[i].x; sy += p[i].y; sz += p[i].z; }
     double dn = (double)n;
@@ -555,6 +568,7 @@ static int contact_case04(const v3* A, int na, const v3* B, v3* res) {
     if (st) return st;
     int C = 0;
     for (int i = 0; i < 2; ++i) if (is_inside_pf(srt, na, B[i])) ++C;
+    COV(C == 0 ? ORC_BR_V2_CASE04_1 : C == 1 ? ORC_BR_V2_CASE04_3 : ORC_BR_V2_CASE04_2);
     if (C == 0) {                                                   /* case_04_1 */
         double sx = 0.0, sy = 0.0, sz = 0.0;
         for (int i = 0; i < na; ++i) { sx += A[i].x; sy += A[i].y; sz += A[i].z; }
@@ -572,16 +586,18 @@ static int contact_v2(const hull_t* a, const hull_t* b, v3 n, v3* res) {
     int n1 = support_set(a, n, SUPPORT_BAND, s1);
     int n2 = support_set(b, vneg(n), SUPPORT_BAND, s2);
     *res = ORIGIN;
-    if (n1 == 1 && n2 == 1) *res = vdiv(vadd(s1[0], s2[0]), 2.0);          /* case_01 */
-    else if (n1 == 1 && n2 >= 2) *res = s1[0];                             /* case_02 */
-    else if (n1 >= 2 && n2 == 1) *res = s2[0];
+    if (n1 == 1 && n2 == 1) { *res = vdiv(vadd(s1[0], s2[0]), 2.0); COV(ORC_BR_V2_CASE01); }   /* case_01 */
+    else if (n1 == 1 && n2 >= 2) { *res = s1[0]; COV(ORC_BR_V2_CASE02); }                    /* case_02 */
+    else if (n1 >= 2 && n2 == 1) { *res = s2[0]; COV(ORC_BR_V2_CASE02B); }
     else if (n1 == 2 && n2 == 2) {                                         /* case_03 */
+        COV(ORC_BR_V2_CASE03);
         v3 f1, f2;
         foot_ll(s1[0], s1[1], s2[0], s2[1], &f1, &f2);
         *res = vdiv(vadd(f1, f2), 2.0);
-    } else if (n1 == 2 && n2 >= 3) return contact_case04(s2, n2, s1, res);
-    else if (n1 >= 3 && n2 == 2) return contact_case04(s1, n1, s2, res);
+    } else if (n1 == 2 && n2 >= 3) { COV(ORC_BR_V2_CASE04); return contact_case04(s2, n2, s1, res); }
+    else if (n1 >= 3 && n2 == 2) { COV(ORC_BR_V2_CASE04B); return contact_case04(s1, n1, s2, res); }
     else if (n1 >= 3 && n2 >= 3) {                                         /* case_05 */
+        COV(ORC_BR_V2_CASE05);
         double sx = 0.0, sy = 0.0, sz = 0.0;
         for (int i = 0; i < n1; ++i) { sx += s1[i].x; sy += s1[i].y; sz += s1[i].z; }
         double dn = (double)n1;
@@ -607,6 +623,7 @@ static int contact_v3(const hull_t* a, const hull_t* b, v3 n, v3* res, v3* nnew)
     v3 q = mk(n.x, n.y, 0.0);
     double nq = norm2(q);
     *nnew = vdiv(q, nq);
+    if (!(nq > 0.0)) COV(ORC_BR_V3_NAN);          /* n = +-z: 0/0 (:447) */
     return 0;
 }
 
@@ -620,7 +637,7 @@ static int gjkepa_pair(int32_t version, double tol_ff, const hull_t* A, const hu
         out->status = GJKEPA_STATUS_BAD_INPUT;
         return 0;
     }
-    if (!sphere_test(A, B)) return 0;                                        /* :76-77 */
+    if (!sphere_test(A, B)) { COV(ORC_BR_SPHERE_MISS); return 0; }           /* :76-77 */
     v3 S[4] = {ORIGIN, ORIGIN, ORIGIN, ORIGIN};   /* fresh THREADPRIVATE SAVE state: row 4 = 0 */
     int st = 0, hit = 0, gjk_it = 0;
     /* --- initial simplex (:82-170) --- */
@@ -628,7 +645,8 @@ static int gjkepa_pair(int32_t version, double tol_ff, const hull_t* A, const hu
     v3 dir;
     for (;;) {
         ++iter;
-        if (iter > INIT_MAXIT) return 0;                                      /* :86-89 */
+        if (iter > INIT_MAXIT) { COV(ORC_BR_INIT_CAP); return 0; }           /* :86-89 */
+        if (iter > 1) COV(ORC_BR_INIT_RETRY);                                   /* :106-112 */
         dir = mk(DIRTAB[iter - 1][0], DIRTAB[iter - 1][1], DIRTAB[iter - 1][2]);
         S[0] = support(A, B, dir);
         dir = vneg(dir);
@@ -637,12 +655,13 @@ static int gjkepa_pair(int32_t version, double tol_ff, const hull_t* A, const hu
     }
     dir = vec_pl(ORIGIN, S[0], S[1]);                                          /* :116 */
     S[2] = support(A, B, dir);
-    if (allclose8(S[2], S[0]) || allclose8(S[2], S[1])) return 0;              /* :123-127 */
+    if (allclose8(S[2], S[0]) || allclose8(S[2], S[1])) { COV(ORC_BR_INIT_S3_COINCIDE); return 0; }   /* :123-127 */
     dir = utzvec(cross(vsub(S[1], S[0]), vsub(S[2], S[1])));                  /* :132-135 */
     v3 VO = vsub(ORIGIN, S[2]);
     double vd = dot(VO, dir);
     if (fabs(vd) < TOL_PT) {                                                   /* :140-148 */
-        if (is_inside_pf(S, 3, ORIGIN)) { hit = 1; goto do_epa; }
+        if (is_inside_pf(S, 3, ORIGIN)) { COV(ORC_BR_INIT_TRI_HIT); hit = 1; goto do_epa; }
+        COV(ORC_BR_INIT_TRI_PLANE);
     }
     if (vd < 0.0) dir = vneg(dir);                                             /* :151 */
     S[3] = support(A, B, dir);                                                 /* :154 */
@@ -650,30 +669,34 @@ static int gjkepa_pair(int32_t version, double tol_ff, const hull_t* A, const hu
         double r;
         st = dist_pf_sign(S[3], S[0], S[1], S[2], &r);                         /* :157 */
         if (st) goto fail;
-        if (fabs(r) < TOL_PT) return 0;
+        if (fabs(r) < TOL_PT) { COV(ORC_BR_INIT_COPLANAR); return 0; }
     }
-    if (is_point_in_simplex(ORIGIN, S)) { hit = 1; goto do_epa; }              /* :164-170 */
+    {
+        int pis = is_point_in_simplex(ORIGIN, S);                              /* :164-170 */
+        if (pis) { COV(pis == 2 ? ORC_BR_INIT_TETRA_ONFACE : ORC_BR_INIT_TETRA_HIT); hit = 1; goto do_epa; }
+    }
     {
         v3 L1[4] = {ORIGIN, ORIGIN, ORIGIN, ORIGIN}, L2[4] = {ORIGIN, ORIGIN, ORIGIN, ORIGIN};
         iter = 0;
         for (;;) {                                                             /* :182-236 */
             ++iter;
             gjk_it = iter;
-            if (iter > GJK_MAXIT) return 0;
+            if (iter > GJK_MAXIT) { COV(ORC_BR_LOOP_CAP); return 0; }
             memcpy(L2, L1, sizeof(L1));
             memcpy(L1, S, sizeof(L1));
             update_simplex(A, B, S);
-            if (norm2(cross(vsub(S[1], S[0]), vsub(S[2], S[1]))) < TOL_PT) return 0;   /* :199-201 */
+            if (norm2(cross(vsub(S[1], S[0]), vsub(S[2], S[1]))) < TOL_PT) { COV(ORC_BR_LOOP_COLLINEAR); return 0; }   /* :199-201 */
             double r;
             st = dist_pf_sign(S[3], S[0], S[1], S[2], &r);                     /* :203 */
             if (st) { out->diag = (uint32_t)(gjk_it & 0xff); goto fail; }
-            if (fabs(r) < TOL_PT) return 0;
-            if (is_point_in_simplex(ORIGIN, S)) { hit = 1; break; }            /* :210-216 */
+            if (fabs(r) < TOL_PT) { COV(ORC_BR_LOOP_COPLANAR); return 0; }       /* :203-206 */
+            const int pis = is_point_in_simplex(ORIGIN, S);                    /* :210-216 */
+            if (pis) { COV(pis == 2 ? ORC_BR_LOOP_ONFACE : ORC_BR_LOOP_HIT); hit = 1; break; }
             int over = 1;                                                      /* :219-234 */
             for (int i = 0; i < 4; ++i) {
                 if (!(allclose8(S[i], L1[i]) || allclose8(S[i], L2[i]))) { over = 0; break; }
             }
-            if (over) return 0;
+            if (over) { COV(ORC_BR_LOOP_CYCLE); return 0; }
         }
     }
 do_epa:
@@ -693,6 +716,7 @@ do_epa:
         else st = GJKEPA_STATUS_BAD_VERSION;
         if (st) goto fail;
         out->colli_type = (int8_t)collision_type(A, B, n, tol_ff);              /* :343 */
+        COV(out->colli_type == 2 ? ORC_BR_TYPE2 : ORC_BR_TYPE1);
         out->penetration_depth = depth;
         out->collision_normal[0] = n.x; out->collision_normal[1] = n.y; out->collision_normal[2] = n.z;
         out->collision_point[0] = pt.x; out->collision_point[1] = pt.y; out->collision_point[2] = pt.z;
@@ -702,6 +726,8 @@ do_epa:
     (void)hit;
     return 0;
 fail: {
+        if (st == GJKEPA_STATUS_DEGENERATE) COV(ORC_BR_DEGENERATE);
+        if (st == GJKEPA_STATUS_BAD_VERSION) COV(ORC_BR_BAD_VERSION);
         uint32_t diag = out->diag;
         zero_record(out);
         out->collision = 1;
@@ -736,6 +762,14 @@ int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
                         const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
                         const int32_t* pairs, int64_t n_pairs,
                         gjkepa_contact_f64* out, int32_t nthreads) {
+    return oracle_gjkepa_batch_cov(version, tol_ff, vert_dtype, verts, hull_off, hull_cnt, pairs, n_pairs, out,
+                                   NULL, nthreads);
+}
+
+int oracle_gjkepa_batch_cov(int32_t version, double tol_ff, int32_t vert_dtype,
+                            const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
+                            const int32_t* pairs, int64_t n_pairs,
+                            gjkepa_contact_f64* out, uint64_t* cov, int32_t nthreads) {
     if (!verts || !hull_off || !hull_cnt || !pairs || !out || n_pairs < 0) return GJKEPA_E_ARG;
     if (vert_dtype != GJKEPA_DTYPE_F32 && vert_dtype != GJKEPA_DTYPE_F64) return GJKEPA_E_ARG;
     int nt = nthreads > 0 ? nthreads : oracle_max_threads();
@@ -753,6 +787,7 @@ int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
             if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
                 zero_record(&out[k]);
                 out[k].status = GJKEPA_STATUS_BAD_INPUT;
+                if (cov) cov[k] = 1ull << ORC_BR_BAD_INPUT;
                 continue;
             }
             if (vert_dtype == GJKEPA_DTYPE_F64) {
@@ -768,7 +803,9 @@ int oracle_gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype,
             }
             A.n = na;
             B.n = nb;
+            g_cov = 0;
             gjkepa_pair(version, tol_ff, &A, &B, H, &out[k]);
+            if (cov) cov[k] = g_cov;
         }
         free(H); free(b1); free(b2);
     }

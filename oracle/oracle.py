@@ -70,6 +70,48 @@ def gjkepa_batch(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0)
     return out
 
 
+# ORC_BR_* bit names (gjkepa_oracle.h), in bit order
+BRANCHES = [
+    "SPHERE_MISS", "INIT_RETRY", "INIT_CAP", "INIT_S3_COINCIDE", "INIT_TRI_HIT", "INIT_TRI_PLANE",
+    "INIT_COPLANAR", "INIT_TETRA_HIT", "INIT_TETRA_ONFACE", "LOOP_CAP", "LOOP_COLLINEAR", "LOOP_COPLANAR",
+    "LOOP_HIT", "LOOP_ONFACE", "LOOP_CYCLE", "IPF_XZ", "EPA_CENTROID", "EPA_FLIP", "EPA_TWO", "EPA_SWALLOW",
+    "EPA_STOP_EQUAL", "EPA_STOP_SHRINK", "EPA_CAP", "DEGENERATE", "BAD_VERSION", "BAD_INPUT",
+    "V1_MID", "V1_B", "V1_A", "V1_MEAN", "V2_CASE01", "V2_CASE02", "V2_CASE02B", "V2_CASE03", "V2_CASE04",
+    "V2_CASE04B", "V2_CASE04_1", "V2_CASE04_2", "V2_CASE04_3", "V2_CASE05", "V2_OVERLAP", "FOOTLL_PARALLEL",
+    "V3_NAN", "TYPE1", "TYPE2",
+]
+BR = {name: i for i, name in enumerate(BRANCHES)}
+
+
+def gjkepa_batch_cov(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0):
+    """gjkepa_batch plus, per pair, the uint64 mask of reference branches taken (bit BR[name])."""
+    verts = np.ascontiguousarray(pool.verts)
+    code = 0 if verts.dtype == np.float32 else 1
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    prs = np.ascontiguousarray(pool.pairs, np.int32).reshape(-1)
+    n = prs.size // 2
+    out = np.zeros(n, REC64)
+    cov = np.zeros(n, np.uint64)
+    lib = load()
+    if not hasattr(lib, "_cov_typed"):
+        vp, i32 = ctypes.c_void_p, ctypes.c_int32
+        lib.oracle_gjkepa_batch_cov.argtypes = [i32, ctypes.c_double, i32, vp, vp, vp, vp, ctypes.c_int64, vp, vp, i32]
+        lib.oracle_gjkepa_batch_cov.restype = ctypes.c_int
+        lib._cov_typed = True
+    rc = lib.oracle_gjkepa_batch_cov(int(version), float(tol_ff), code, verts.ctypes.data, off.ctypes.data,
+                                     cnt.ctypes.data, prs.ctypes.data, n, out.ctypes.data, cov.ctypes.data,
+                                     int(nthreads))
+    assert rc == 0
+    return out, cov
+
+
+def branch_histogram(cov) -> dict:
+    """{branch name: number of pairs that took it}."""
+    cov = np.asarray(cov, np.uint64)
+    return {name: int(((cov >> np.uint64(i)) & np.uint64(1)).sum()) for i, name in enumerate(BRANCHES)}
+
+
 def max_threads() -> int:
     return int(load().oracle_max_threads())
 
