@@ -5,10 +5,13 @@ Workload (N=1) = BASELINE config C2: 2^20 random 32-vertex convex-hull pairs, fp
 version_=2, TOL_FF_=1.0, hull B centre offset r ~ U[0, 2.5] (seed 0x6A4B5C1D).
 A "step" is one pass of the hot path (gjkepa_batch_device: the tiered GJK/EPA kernels) over the
 whole batch, with hulls, pair list and output already resident in HBM.  For N > 1 each rank owns
-a contiguous shard of `--pairs-per-gpu` pairs (weak scaling) and every step's contact records are
-all-gathered over xGMI with RCCL (config C3's exchange).  The gather of step i runs on RCCL's
-stream while step i+1's kernels run (two record buffers); the timed region ends after the last
-gather has completed, so every step's exchange is inside it (`--no-overlap`: gather in line).
+a contiguous shard of `--pairs-per-gpu` pairs (weak scaling; the library's gjkepa_shard_range) and
+every step's contact records are all-gathered over xGMI by the library's RCCL communicator
+(gjkepa_comm_* / gjkepa_allgather_records_device: config C3's exchange).  The gather of step i runs
+on its own stream while step i+1's kernels run (two record buffers, gathered in place); the timed
+region ends after the last gather has completed, so every step's exchange is inside it.
+torch.distributed (gloo) is the control plane only: RCCL id broadcast, barriers, max over ranks.
+`--backend gloo` is the one-GPU rehearsal: ranks may share a device, records gathered via host.
 
 Extra legs (not timed in `value`): the roofline of the dominant kernel from HIP events on the
 launch stream, and on rank 0 at N=1 a CPU baseline — the oracle restatement (kind "port") over a
@@ -70,12 +73,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
     ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: the config's size")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 record exchange: nccl = the library's RCCL all-gather, gloo = host-staged rehearsal")
     ap.add_argument("--version", type=int, default=2)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather for N>1")
-    ap.add_argument("--no-overlap", action="store_true", help="N>1: gather synchronously instead of overlapping it "
-                                                                "with the next step's kernels")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
     ap.add_argument("--no-warm-leg", action="store_true", help="skip the warm-start side measurement")
@@ -96,22 +98,18 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")          # control plane; the data path is the library's RCCL
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))   # gloo rehearsal: ranks may share a GPU
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", torch.cuda.current_device())
-    host_coll = dist is not None and args.backend != "nccl"     # gloo: collectives staged through host memory
     lib = gjkepa.load()
 
     nmin, nmax, rmax, n_default, desc = CONFIGS[args.config]
     n = args.pairs_per_gpu or n_default
     prec = gjkepa.PREC_F64 if args.precision == "f64" else gjkepa.PREC_F32
     rec_bytes = lib.gjkepa_record_bytes(prec)
-    first, _ = shard.shard_range(n * world, world, rank)
+    first, _ = shard.shard_range(n * world, world, rank)      # gjkepa_shard_range
     pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax, first_pair=first, dtype=np.float32)
     verts = torch.from_numpy(pool.verts).to(dev)
     off = torch.from_numpy(pool.hull_off).to(dev)
@@ -120,11 +118,14 @@ def main():
     out = torch.zeros(n * rec_bytes, dtype=torch.uint8, device=dev)
     ws_bytes = gjkepa.workspace_bytes(n)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
-    # N > 1: every step's records are all-gathered (shard.RecordExchange); on RCCL step i's gather
-    # overlaps step i+1's kernels (two record buffers), on gloo it is staged through host memory
-    ex = None
+    # N > 1: every step's records are all-gathered (shard.RecordExchange); with the library's RCCL
+    # communicator step i's gather overlaps step i+1's kernels (two record buffers), on gloo it is
+    # staged through host memory
+    ex, comm = None, None
     if world > 1 and not args.no_gather:
-        ex = shard.RecordExchange(n * rec_bytes, world, dev, overlap=not args.no_overlap, host_staged=host_coll)
+        if args.backend == "nccl":
+            comm = shard.make_comm(world, rank, dev.index)
+        ex = shard.RecordExchange(n * rec_bytes, world, rank, dev, prec, comm=comm)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -135,14 +136,14 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
-        o = ex.buffer() if ex else out       # a reused buffer first waits for the gather that read it
+        o = ex.buffer(stream) if ex else out   # a reused buffer first waits for the gather that read it
         if i is not None:
             ev[i][0].record(stream)
         launch(prec, o)
         if i is not None:
             ev[i][1].record(stream)
         if ex:
-            ex.submit()
+            ex.submit(stream)
 
     def drain():
         if ex:
@@ -166,7 +167,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
     if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if host_coll else dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     ms_per_step = 1e3 * elapsed / args.steps
@@ -212,8 +213,8 @@ def main():
                                f"version_={args.version}, TOL_FF_=1.0, hull B offset r~U[0,{rmax}]",
                    "hull_vertices": [nmin, nmax],
                    "pairs_per_gpu": n, "total_pairs": total_pairs, "seed": SEED,
-                   "parallelism": f"shard{world}" + ("" if ex is None else "+allgather_overlapped" if ex.overlap
-                                                       else "+allgather"),
+                   "parallelism": f"shard{world}" + ("" if ex is None else "+rccl_allgather_overlapped" if ex.overlap
+                                                       else "+gloo_allgather_host_staged"),
                    "vert_storage": "f32", "record_bytes": rec_bytes},
         "roofline": roofline,
         "hit_rate": round(hit_rate, 4), "epa_iters_mean": round(epa_mean, 2), "status_counts": status_counts,
@@ -306,6 +307,8 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -20,6 +20,7 @@
 #include "hull_kernel.h"
 #include "broadphase_kernel.h"
 #include "contacts_kernel.h"
+#include "capi_internal.h"
 
 namespace {
 
@@ -169,6 +170,10 @@ bool valid_enums(int32_t vert_dtype, int32_t precision) {
 }
 
 }  // namespace
+
+namespace gjkepa_internal {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace gjkepa_internal
 
 extern "C" {
 

@@ -5,7 +5,8 @@
 !   GJKEPA        unchanged public signature (GCLIB_GJKEPA.f90:39-52).  One pair, answered by
 !                 the HIP kernels through the C-ABI (include/gjkepa.h: gjkepa_query).
 !   GJKEPA_BATCH  the batched form: a pooled hull set and a pair list, replacing the caller's
-!                 `!$OMP PARALLEL DO ... CALL GJKEPA` loop with one GPU submission.
+!                 `!$OMP PARALLEL DO ... CALL GJKEPA` loop with one GPU submission; with the
+!                 optional devices_ list, one submission per GPU of the node (contiguous shards).
 !   GJKEPA_LAST_STATUS  per-thread status of the last GJKEPA call (the reference PAUSEs/STOPs
 !                 instead, :300-301, :337-339, :1370-1372; here the call returns and reports).
 !   GJKEPA_BROADPHASE  the pairs (a < b) of a pooled hull set that pass the reference's own first
@@ -69,6 +70,20 @@ MODULE GCLIB_GJKEPA
             TYPE(contact_f64), INTENT(OUT) :: out(*)
             INTEGER(C_INT) :: c_gjkepa_batch
         END FUNCTION c_gjkepa_batch
+
+        FUNCTION c_gjkepa_batch_multi(version, tol_ff, vert_dtype, precision, verts, n_vert_scalars, &
+                                      hull_off, hull_cnt, n_hulls, pairs, n_pairs, out, devices, ndev) &
+                                      BIND(C, NAME="gjkepa_batch_multi")
+            IMPORT :: C_INT32_T, C_INT64_T, C_DOUBLE, C_INT, contact_f64
+            INTEGER(C_INT32_T), VALUE :: version, vert_dtype, precision, ndev
+            REAL(C_DOUBLE), VALUE     :: tol_ff
+            REAL(C_DOUBLE), INTENT(IN) :: verts(*)
+            INTEGER(C_INT64_T), VALUE :: n_vert_scalars, n_hulls, n_pairs
+            INTEGER(C_INT64_T), INTENT(IN) :: hull_off(*)
+            INTEGER(C_INT32_T), INTENT(IN) :: hull_cnt(*), pairs(*), devices(*)
+            TYPE(contact_f64), INTENT(OUT) :: out(*)
+            INTEGER(C_INT) :: c_gjkepa_batch_multi
+        END FUNCTION c_gjkepa_batch_multi
 
         FUNCTION c_gjkepa_broadphase(vert_dtype, verts, n_vert_scalars, hull_off, hull_cnt, n_hulls, &
                                      pairs, max_pairs, n_pairs, dev) BIND(C, NAME="gjkepa_broadphase")
@@ -150,10 +165,13 @@ CONTAINS
     !                    as x(1:n), y(1:n), z(1:n)  (1-based offsets, n = hull_cnt_(h))
     !   pairs_(2,np)     1-based hull indices (p1_, p2_) of each pair
     !   outputs          per pair, same meaning as GJKEPA's INTENT(OUT) arguments, plus status_
+    !   devices_         OPTIONAL 0-based GPU list: the pairs split into SIZE(devices_) contiguous
+    !                    shards, one per device, run concurrently (gjkepa_batch_multi); results are
+    !                    identical to one device.  Absent: the device of GJKEPA_SET_DEVICE.
     !-----------------------------------------------------------------------------------------
     SUBROUTINE GJKEPA_BATCH(version_, TOL_FF_, verts_, hull_off_, hull_cnt_, pairs_, &
                             collision_, colliType_, nearest_points_, collision_normal_, &
-                            collision_point_, penetration_depth_, status_)
+                            collision_point_, penetration_depth_, status_, devices_)
         INTEGER*4, INTENT(IN)  :: version_
         REAL*8,    INTENT(IN)  :: TOL_FF_
         REAL*8,    INTENT(IN)  :: verts_(:)
@@ -167,6 +185,7 @@ CONTAINS
         REAL*8,    INTENT(OUT) :: collision_point_(:,:)      ! (3,np)
         REAL*8,    INTENT(OUT) :: penetration_depth_(:)
         INTEGER*4, INTENT(OUT) :: status_(:)
+        INTEGER*4, INTENT(IN), OPTIONAL :: devices_(:)
         TYPE(contact_f64), ALLOCATABLE :: rec(:)
         REAL(C_DOUBLE), ALLOCATABLE :: v(:)
         INTEGER(C_INT64_T), ALLOCATABLE :: off(:)
@@ -181,8 +200,14 @@ CONTAINS
         off = hull_off_ - 1                     ! 0-based scalar offsets for the C-ABI
         cnt = hull_cnt_
         prs = RESHAPE(pairs_ - 1, [INT(2 * np)])
-        rc = c_gjkepa_batch(INT(version_, C_INT32_T), TOL_FF_, 1_C_INT32_T, 1_C_INT32_T, v, &
-                            INT(SIZE(verts_), C_INT64_T), off, cnt, nh, prs, np, rec, device)
+        IF (PRESENT(devices_)) THEN
+            rc = c_gjkepa_batch_multi(INT(version_, C_INT32_T), TOL_FF_, 1_C_INT32_T, 1_C_INT32_T, v, &
+                                      INT(SIZE(verts_), C_INT64_T), off, cnt, nh, prs, np, rec, &
+                                      INT(devices_, C_INT32_T), INT(SIZE(devices_), C_INT32_T))
+        ELSE
+            rc = c_gjkepa_batch(INT(version_, C_INT32_T), TOL_FF_, 1_C_INT32_T, 1_C_INT32_T, v, &
+                                INT(SIZE(verts_), C_INT64_T), off, cnt, nh, prs, np, rec, device)
+        END IF
         IF (rc /= 0) THEN
             CALL report(rc, "GJKEPA_BATCH")
             collision_ = .FALSE.; colliType_ = 0; nearest_points_ = 0.D0

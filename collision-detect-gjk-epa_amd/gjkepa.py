@@ -33,8 +33,10 @@ EXPORTS = (
     "gjkepa_hull_face_capacity", "gjkepa_hull_batch", "gjkepa_hull_batch_device", "gjkepa_synth_clouds",
     "gjkepa_broadphase_workspace_bytes", "gjkepa_broadphase", "gjkepa_broadphase_device", "gjkepa_synth_scene",
     "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
-    "gjkepa_collide",
+    "gjkepa_collide", "gjkepa_shard_range", "gjkepa_batch_multi", "gjkepa_comm_unique_id", "gjkepa_comm_init",
+    "gjkepa_comm_destroy", "gjkepa_comm_backend", "gjkepa_allgather_records_device",
 )
+COMM_ID_BYTES = 128
 HULL_MAX_POINTS = 256
 
 REC64 = np.dtype([
@@ -120,6 +122,20 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_collide.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                    c_vp, c_i32]
     lib.gjkepa_collide.restype = ctypes.c_int
+    lib.gjkepa_shard_range.argtypes = [c_i64, c_i32, c_i32, c_vp, c_vp]
+    lib.gjkepa_shard_range.restype = ctypes.c_int
+    lib.gjkepa_batch_multi.argtypes = [c_i32, c_dbl, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                       c_vp, c_i32]
+    lib.gjkepa_batch_multi.restype = ctypes.c_int
+    lib.gjkepa_comm_unique_id.argtypes = [c_vp]
+    lib.gjkepa_comm_unique_id.restype = ctypes.c_int
+    lib.gjkepa_comm_init.argtypes = [c_vp, c_i32, c_i32, c_vp, c_i32]
+    lib.gjkepa_comm_init.restype = ctypes.c_int
+    lib.gjkepa_comm_destroy.argtypes = [c_vp]
+    lib.gjkepa_comm_destroy.restype = ctypes.c_int
+    lib.gjkepa_comm_backend.restype = ctypes.c_char_p
+    lib.gjkepa_allgather_records_device.argtypes = [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp]
+    lib.gjkepa_allgather_records_device.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -256,12 +272,73 @@ def gjkepa_batch_warm_device(version: int, tol_ff: float, vert_dtype: int, preci
                              hull_off_ptr: int, hull_cnt_ptr: int, pairs_ptr: int, n_pairs: int, out_ptr: int,
                              ws_ptr: int, ws_bytes: int, warm_ptr: int, stream: int = 0) -> None:
     """gjkepa_batch_device with a per-pair warm-start slot array (device uint32[4 * n_pairs], in/out;
-    0xFFFFFFFF = none): persistent pairs whose last simplex still encloses the origin skip GJK, and
-    pairs that missed last time first try the hull-centre separating axis."""
+    0xFFFFFFFF = none): persistent pairs whose last simplex still encloses the origin skip GJK."""
     rc = load().gjkepa_batch_warm_device(int(version), float(tol_ff), int(vert_dtype), int(precision), verts_ptr,
                                          hull_off_ptr, hull_cnt_ptr, pairs_ptr, int(n_pairs), out_ptr, ws_ptr,
                                          int(ws_bytes), warm_ptr, stream or None)
     _check(rc, "gjkepa_batch_warm_device")
+
+
+# ---- multi-GPU (SURVEY.md §8 row e; include/gjkepa.h gjkepa_shard_range / _batch_multi / _comm_*) ------
+def shard_range(n_pairs: int, world: int, rank: int) -> tuple[int, int]:
+    """(first, count): the contiguous shard of pairs `rank` of `world` owns (the library's rule)."""
+    first, count = ctypes.c_int64(), ctypes.c_int64()
+    _check(load().gjkepa_shard_range(int(n_pairs), int(world), int(rank), ctypes.byref(first), ctypes.byref(count)),
+           "gjkepa_shard_range")
+    return first.value, count.value
+
+
+def gjkepa_batch_multi(pool: HullPool, devices, version: int = 2, tol_ff: float = 1.0,
+                       precision: int = PREC_F64) -> np.ndarray:
+    """One process driving several devices: pool's pairs in contiguous shards, shard s on devices[s];
+    returns every record in pair order (bit-identical to gjkepa_batch)."""
+    lib = load()
+    out = np.zeros(pool.n_pairs, dtype=record_dtype(precision))
+    verts = np.ascontiguousarray(pool.verts)
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    prs = np.ascontiguousarray(pool.pairs, np.int32).reshape(-1)
+    dev = np.ascontiguousarray(devices, np.int32)
+    rc = lib.gjkepa_batch_multi(int(version), float(tol_ff), pool.dtype_code, int(precision), _ptr(verts), verts.size,
+                                _ptr(off), _ptr(cnt), cnt.size, _ptr(prs), pool.n_pairs, _ptr(out), _ptr(dev),
+                                dev.size)
+    _check(rc, "gjkepa_batch_multi")
+    return out
+
+
+class Comm:
+    """RCCL communicator of the contact-record exchange, one process per device (config C3).
+    Rank 0 calls ``Comm.unique_id()``; the caller broadcasts those bytes (e.g. torch.distributed);
+    every rank then builds ``Comm(world, rank, uid, device)``."""
+
+    def __init__(self, world: int, rank: int, uid: bytes, device: int):
+        if len(uid) != COMM_ID_BYTES:
+            raise GjkEpaError("unique id must be COMM_ID_BYTES bytes")
+        self.world, self.rank, self.device = world, rank, device
+        self._h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _check(load().gjkepa_comm_init(ctypes.byref(self._h), int(world), int(rank), buf, int(device)),
+               "gjkepa_comm_init")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        _check(load().gjkepa_comm_unique_id(buf), "gjkepa_comm_unique_id")
+        return buf.raw
+
+    @staticmethod
+    def backend() -> str:
+        return load().gjkepa_comm_backend().decode()
+
+    def allgather_records(self, precision: int, shard_ptr: int, all_ptr: int, count: int, stream: int = 0) -> None:
+        """Every rank's `count` records (device pointer) into all_ptr[world * count], rank order; async."""
+        _check(load().gjkepa_allgather_records_device(self._h, int(precision), shard_ptr, all_ptr, int(count),
+                                                      stream or None), "gjkepa_allgather_records_device")
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().gjkepa_comm_destroy(self._h), "gjkepa_comm_destroy")
+            self._h = ctypes.c_void_p()
 
 
 def version_string() -> str:

@@ -53,6 +53,7 @@ extern "C" {
 #define GJKEPA_E_HIP        -2  /* HIP runtime error (see gjkepa_last_error) */
 #define GJKEPA_E_NODEVICE   -3  /* no usable gfx950 device */
 #define GJKEPA_E_WORKSPACE  -4  /* device workspace too small */
+#define GJKEPA_E_COMM       -5  /* RCCL unavailable or a collective failed (see gjkepa_last_error) */
 
 /* ---- enums --------------------------------------------------------------------------------- */
 #define GJKEPA_DTYPE_F32 0      /* vertex storage dtype */
@@ -264,6 +265,43 @@ int gjkepa_collide(int32_t version, double tol_ff, int32_t vert_dtype, int32_t p
                    const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
                    int32_t* pairs, void* out, int64_t max_contacts,
                    int64_t* n_contacts, int64_t* n_candidates, int32_t device);
+
+/* ---- multi-GPU (SURVEY.md §8 row e) ---------------------------------------------------------------
+ * Pairs are independent: a job splits into contiguous shards of pairs, one per device, with no
+ * exchange during compute.  The reference's own parallelism is the caller's OpenMP loop over GJKEPA
+ * (GCLIB_GJKEPA.f90:9, :16, :55-60); these entries replace it across the GPUs of a node.
+ *
+ * gjkepa_shard_range: rank r of `world` owns pairs [first, first + count); shards differ by at most
+ * one pair (the first n_pairs % world ranks get one more). */
+int gjkepa_shard_range(int64_t n_pairs, int32_t world, int32_t rank, int64_t* first, int64_t* count);
+
+/* One process, several devices (host buffers, blocking): gjkepa_batch's arguments plus a device list.
+ * Shard s (gjkepa_shard_range over ndev) runs on devices[s] from its own host thread; only the hulls
+ * the shard references are copied to that device; its records land at out[first .. first + count),
+ * so `out` holds every record in pair order — bit-identical to one gjkepa_batch call. */
+int gjkepa_batch_multi(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
+                       const void* verts, int64_t n_vert_scalars,
+                       const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
+                       const int32_t* pairs, int64_t n_pairs,
+                       void* out, const int32_t* devices, int32_t ndev);
+
+/* One process per device (config C3): an RCCL communicator for the contact-record exchange.
+ * Rank 0 creates the id (gjkepa_comm_unique_id), the caller broadcasts its GJKEPA_COMM_ID_BYTES bytes
+ * (MPI_Bcast, torch.distributed, a file ...), every rank calls gjkepa_comm_init.  RCCL is bound at
+ * run time (the copy already in the process, else librccl.so.1); GJKEPA_E_COMM if it is absent. */
+#define GJKEPA_COMM_ID_BYTES 128
+typedef struct gjkepa_comm gjkepa_comm;
+int gjkepa_comm_unique_id(void* id);
+int gjkepa_comm_init(gjkepa_comm** comm, int32_t world, int32_t rank, const void* id, int32_t device);
+int gjkepa_comm_destroy(gjkepa_comm* comm);
+/* Which RCCL the library bound ("process (...)", "librccl.so.1", or "unavailable"). */
+const char* gjkepa_comm_backend(void);
+
+/* All-gather of every rank's `count` contact records (device buffers; equal shards) into
+ * all_records[world * count] in rank order: one ncclAllGather on `stream` (asynchronous; xGMI).
+ * In place when shard_records == all_records + rank * count records. */
+int gjkepa_allgather_records_device(gjkepa_comm* comm, int32_t precision, const void* shard_records,
+                                    void* all_records, int64_t count, void* stream);
 
 /* Last error message of the calling thread ("" if none). */
 const char* gjkepa_last_error(void);

@@ -52,6 +52,15 @@ PROGRAM test_dropin
             bnp(1, :, i), bnp(2, :, i)
     END DO
 
+    ! the device-list form (gjkepa_batch_multi): same records as the one-device submission
+    CALL GJKEPA_BATCH(2, 1.D-3, verts, hoff, hcnt, prs, ohit, btyp, bnp, on, bp, odep, bst, devices_=[0])
+    nfail = 0
+    DO i = 1, 12
+        IF (ohit(i) .NEQV. bhit(i)) nfail = nfail + 1
+        IF (odep(i) /= bd(i) .OR. ANY(on(:, i) /= bn(:, i))) nfail = nfail + 1
+    END DO
+    WRITE(*, '(A,I4)') 'MULTI_MISMATCH', nfail
+
     ! the reference's caller pattern: OpenMP loop over pairs, each thread calling GJKEPA
     !$OMP PARALLEL DO PRIVATE(B, hit, typ, npt, nrm, cpt, dep) SCHEDULE(DYNAMIC)
     DO i = 1, 12

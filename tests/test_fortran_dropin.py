@@ -35,6 +35,8 @@ def test_fortran_gjkepa_matches_oracle(orc):
         assert np.all((vals == want) | both_nan), (f, want)
     mism = [ln for ln in out.stdout.splitlines() if ln.startswith("OMP_MISMATCH")]
     assert mism and int(mism[0].split()[1]) == 0, "OpenMP callers disagree with the batched entry"
+    mm = [ln for ln in out.stdout.splitlines() if ln.startswith("MULTI_MISMATCH")]
+    assert mm and int(mm[0].split()[1]) == 0, "GJKEPA_BATCH(devices_=...) disagrees with the one-device entry"
 
 
 QH_EXE = os.path.join(ROOT, "tests", "fortran", "build", "test_quickhull")

@@ -1,0 +1,78 @@
+"""Multi-GPU product path on the GPU (SURVEY.md §8 row e, config C3).
+
+- C3 per-rank workload: each of two ranks owns 2^21 C2-distribution pairs at first_pair = r * 2^21
+  (the library's shard rule); each shard, run through the C-ABI on the GPU, is byte-identical to the
+  matching half of one contiguous 2^22-pair run and to the oracle on a subsample.
+- gjkepa_batch_multi (one process, a device list) equals gjkepa_batch; the box has one GPU, so the
+  list holds device 0 (the shard / rebase / thread path is the same for any length).
+- The library's RCCL communicator (world 1 here; the driver's 8-GPU run exercises world 8): the
+  in-place and out-of-place all-gather of records returns them unchanged.
+"""
+import numpy as np
+import pytest
+
+import gjkepa
+
+pytestmark = pytest.mark.gpu
+SEED = 0x6A4B5C1D
+PER_RANK = 1 << 21
+
+
+def _bytes(a):
+    return a.view(np.uint8).reshape(len(a), -1)
+
+
+def test_c3_rank_shards_match_contiguous_run_and_oracle(orc):
+    whole = gjkepa.synth_pairs(SEED, 2 * PER_RANK, 32, 32, 2.5)
+    ref = gjkepa.gjkepa_batch(whole, 2, 1.0)
+    for rank in range(2):
+        first, count = gjkepa.shard_range(2 * PER_RANK, 2, rank)
+        assert (first, count) == (rank * PER_RANK, PER_RANK)
+        pool = gjkepa.synth_pairs(SEED, count, 32, 32, 2.5, first_pair=first)
+        got = gjkepa.gjkepa_batch(pool, 2, 1.0)
+        assert got.tobytes() == ref[first:first + count].tobytes(), rank
+        sub = np.arange(0, count, 97)                      # oracle on a ~21.6k-pair subsample
+        spool = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[sub])
+        o = orc.gjkepa_batch(spool, 2, 1.0)
+        assert got[sub].tobytes() == o.tobytes(), rank
+
+
+@pytest.mark.parametrize("lo,hi", [(32, 32), (8, 256)])
+def test_batch_multi_matches_batch(lo, hi):
+    pool = gjkepa.synth_pairs(SEED, 50000, lo, hi, 2.5)
+    a = gjkepa.gjkepa_batch(pool, 2, 1.0)
+    b = gjkepa.gjkepa_batch_multi(pool, [0], 2, 1.0)
+    assert a.tobytes() == b.tobytes()
+
+
+def test_batch_multi_shared_hull_pool(orc):
+    """A pool whose pairs share hulls out of order (a broad-phase list): each shard copies only the
+    hull range it references, rebased; results equal the oracle."""
+    rng = np.random.default_rng(3)
+    hulls = gjkepa.synth_pairs(SEED, 300, 8, 64, 2.5)
+    prs = rng.integers(0, 600, size=(4000, 2)).astype(np.int32)
+    pool = gjkepa.HullPool(hulls.verts, hulls.hull_off, hulls.hull_cnt, prs)
+    g = gjkepa.gjkepa_batch_multi(pool, [0], 2, 1.0)
+    assert g.tobytes() == orc.gjkepa_batch(pool, 2, 1.0).tobytes()
+
+
+def test_rccl_comm_world1_allgather():
+    import torch
+
+    dev = torch.device("cuda", 0)
+    uid = gjkepa.Comm.unique_id()
+    comm = gjkepa.Comm(1, 0, uid, 0)
+    try:
+        pool = gjkepa.synth_pairs(SEED, 4096, 32, 32, 2.5)
+        recs = gjkepa.gjkepa_batch(pool, 2, 1.0)
+        src = torch.from_numpy(_bytes(recs).reshape(-1).copy()).to(dev)
+        dst = torch.zeros_like(src)
+        s = torch.cuda.current_stream(dev)
+        comm.allgather_records(gjkepa.PREC_F64, src.data_ptr(), dst.data_ptr(), len(recs), s.cuda_stream)
+        comm.allgather_records(gjkepa.PREC_F64, src.data_ptr(), src.data_ptr(), len(recs), s.cuda_stream)  # in place
+        torch.cuda.synchronize(dev)
+        assert dst.cpu().numpy().tobytes() == recs.tobytes()
+        assert src.cpu().numpy().tobytes() == recs.tobytes()
+    finally:
+        comm.close()
+    assert gjkepa.Comm.backend() != "unavailable"
