@@ -66,6 +66,34 @@ def moved_copy(pool, delta: float, seed: int) -> np.ndarray:
     return v.astype(pool.verts.dtype)
 
 
+def host_cpus() -> dict:
+    """Host cores the CPU baseline may use: the process's affinity set, capped by a cgroup CPU quota
+    (a GPU box exposes the whole machine in os.cpu_count() but grants a share of it), and the CPU model."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    usable = min(aff, quota) if quota else aff
+    if env:
+        usable = min(usable, env)
+    return {"usable": usable, "nproc": nproc, "affinity": aff, "cgroup": quota, "model": model,
+            "omp_num_threads": env or None}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,13 +212,16 @@ def main():
     bpq = algorithmic_bytes_per_query(float(pool.hull_cnt.sum()) / n, 4, rec_bytes)
     achieved = n * bpq / (kern_ms * 1e-3) / 1e9
     # HBM traffic and VALU issue of the same chain from the committed PMC run (tools/pmc.sh +
-    # tools/pmc_report.py, keyed by precision/config/batch size); null when none matches
-    traffic, valu = None, None
+    # tools/pmc_report.py), keyed by precision/config/batch size and stamped with the library's
+    # source hash; null unless that hash is the one this process loaded (no figures from another build)
+    traffic, valu, pmc_src = None, None, None
+    lib_src = gjkepa.source_hash()
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof)).get(f"{args.precision}_{args.config}_{n}")
-            if pj:
+            if pj and pj.get("src") == lib_src:
+                pmc_src = pj["src"]
                 traffic = pj["bytes_per_launch"]
                 if pj.get("valu_instr"):
                     valu = {"instr_per_query": round(pj["valu_instr_per_query"], 1),
@@ -198,11 +229,12 @@ def main():
                             "issue_frac_live": round(pj["valu_instr"] * 2.0 / (1024 * kern_ms * 1e-3 * 2.4e9), 4),
                             "note": "SQ_INSTS_VALU priced at the 2-cycle wave64 issue slot vs 1024 SIMDs x kernel time x 2.4 GHz"}
         except Exception:
-            traffic, valu = None, None
+            traffic, valu, pmc_src = None, None, None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic, "valu_issue": valu,
                 "bytes_per_query": round(bpq, 1), "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
-                "kernel": "gjk + epa + contact kernel tiers (one launch chain; HIP events on the launch stream)"}
+                "kernel": "gjk + epa + contact kernel tiers (one launch chain; HIP events on the launch stream)",
+                "pmc_src": pmc_src}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "M queries/s", "n_gpus": world,
@@ -286,7 +318,8 @@ def main():
         import oracle  # checker / CPU baseline only
         m = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
         sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:m])
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+        host = host_cpus()
+        threads = host["usable"]
         oracle.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:256]),
                             args.version, 1.0, threads)
         t = time.perf_counter()
@@ -296,7 +329,14 @@ def main():
             "value": round(m / ct / 1e6, 4), "unit": "M queries/s", "cores": threads, "kind": "port",
             "sample": f"first {m} pairs of the same {args.config} batch, fp64 oracle restatement (oracle/gjkepa_oracle.c), "
                       f"OpenMP dynamic over pairs, {ct:.2f} s wall",
+            "cpu_model": host["model"], "nproc": host["nproc"], "affinity": host["affinity"],
+            "cgroup_cpus": host["cgroup"],
         }
+        # one core, for a per-core figure (a bounded sample: ~1/64 of the pairs the threaded leg ran)
+        m1 = max(256, m // max(threads, 1) // 4)
+        t = time.perf_counter()
+        oracle.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:m1]), args.version, 1.0, 1)
+        result["cpu_baseline"]["per_core"] = {"value": round(m1 / (time.perf_counter() - t) / 1e6, 5), "pairs": m1}
         if prec == gjkepa.PREC_F64:
             g = recs[:m]
             same = (g.tobytes() == cref.tobytes())

@@ -190,17 +190,20 @@ int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
 
 const char* gjkepa_last_error(void) { return g_err.c_str(); }
 
+#ifndef GJKEPA_SRC_HASH
+#define GJKEPA_SRC_HASH "unknown"
+#endif
 const char* gjkepa_version_string(void) {
     static char buf[640];
     std::snprintf(buf, sizeof(buf),
                   "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
                   "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
-                  "-O3 -ffp-contract=off",
+                  "-O3 -ffp-contract=off; src %s",
                   GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
                   GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP,
                   GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
-                  GJKEPA_C1_K);
+                  GJKEPA_C1_K, GJKEPA_SRC_HASH);
     return buf;
 }
 

@@ -345,6 +345,11 @@ def version_string() -> str:
     return load().gjkepa_version_string().decode()
 
 
+def source_hash() -> str:
+    """The hash of the sources the loaded library was built from (Makefile SRCHASH)."""
+    return version_string().rsplit("src ", 1)[-1].strip()
+
+
 # ---- batched convex hulls (SURVEY.md §8 row f1; include/gjkepa.h gjkepa_hull_batch) ----------------
 @dataclass
 class CloudPool:

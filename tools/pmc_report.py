@@ -8,6 +8,8 @@ FETCH_SIZE counts half the bytes of wide reads, so traffic = (2 * FETCH_SIZE + W
 VALU issue: SQ_INSTS_VALU wave-instructions; `valu_issue_frac` prices each at the 2-cycle wave64
 issue slot (32 lanes/clock) against 1024 SIMDs x the chain's kernel time x 2.4 GHz (fp64 ops take
 longer, so this is a lower bound on VALU-pipe occupancy).
+The entry carries the library source hash the passes ran (gjkepa_version_string); bench.py uses
+it only when the loaded library has the same hash.
 usage: python tools/pmc_report.py <gpurun_out tag> <key> <n_pairs>  (merges into profiles/pmc_traffic.json)"""
 import collections
 import csv
@@ -47,7 +49,15 @@ def main():
         tot.update(m)
     traffic = (2.0 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0
     secs = tot["seconds"]
+    srcs = set()
+    for f in sorted(glob.glob(f"{base}/p*.json")):
+        for line in open(f):
+            if line.startswith("{"):
+                srcs.add(json.loads(line)["lib"].rsplit("src ", 1)[-1].strip())
+    if len(srcs) != 1:
+        sys.exit(f"PMC passes disagree on (or lack) the library source hash: {srcs}")
     entry = {
+        "src": srcs.pop(),
         "bytes_per_launch": traffic,
         "fetch_bytes_corrected": 2.0 * tot["FETCH_SIZE"] * 1024.0,
         "write_bytes": tot["WRITE_SIZE"] * 1024.0,
