@@ -194,16 +194,19 @@ const char* gjkepa_last_error(void) { return g_err.c_str(); }
 #define GJKEPA_SRC_HASH "unknown"
 #endif
 const char* gjkepa_version_string(void) {
-    static char buf[640];
+    static char buf[800];
     std::snprintf(buf, sizeof(buf),
                   "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
                   "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
+                  "waves/SIMD G%d%d E%d%d%d%d%d C%d%d; LDS-hull G%d%d E%d%d%d%d%d C%d%d; "
                   "-O3 -ffp-contract=off; src %s",
                   GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
                   GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP,
                   GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
-                  GJKEPA_C1_K, GJKEPA_SRC_HASH);
+                  GJKEPA_C1_K, GJKEPA_G0_MINW, GJKEPA_G1_MINW, GJKEPA_E0_MINW, GJKEPA_E1_MINW, GJKEPA_E2_MINW,
+                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH, GJKEPA_E0_LH,
+                  GJKEPA_E1_LH, GJKEPA_E2_LH, GJKEPA_E3_LH, GJKEPA_E4_LH, GJKEPA_C0_LH, GJKEPA_C1_LH, GJKEPA_SRC_HASH);
     return buf;
 }
 

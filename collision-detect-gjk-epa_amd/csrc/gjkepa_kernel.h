@@ -48,7 +48,7 @@
 #define GJKEPA_E0_FCAP 64
 #endif
 #ifndef GJKEPA_E0_MINW
-#define GJKEPA_E0_MINW 2
+#define GJKEPA_E0_MINW 3        // with GJKEPA_E0_LH: 160 VGPRs, no spills; LDS holds 11 waves/CU
 #endif
 #ifndef GJKEPA_E0_REFILL
 #define GJKEPA_E0_REFILL 2      // refill a wave's groups once this many are idle (0: per-round kernel)
@@ -99,7 +99,7 @@
 #define GJKEPA_E3_FCAP 208
 #endif
 #ifndef GJKEPA_E3_MINW
-#define GJKEPA_E3_MINW 1
+#define GJKEPA_E3_MINW 2
 #endif
 #ifndef GJKEPA_E4_G
 #define GJKEPA_E4_G 64
@@ -135,14 +135,49 @@
 #ifndef GJKEPA_C1_MINW
 #define GJKEPA_C1_MINW 1
 #endif
+#ifndef GJKEPA_EPA_PLACE
+#define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
+#endif
+#ifndef GJKEPA_LDS_SKEW
+#define GJKEPA_LDS_SKEW 1           // pad LDS coordinate columns and skew group images across banks (0: A/B off)
+#endif
 #ifndef GJKEPA_AXIS_REJECT
 #define GJKEPA_AXIS_REJECT 0        // diagnostic A/B only, never the product build: GJK answers "miss"
                                     // when the centre axis separates the hulls.  Not parity-safe: the
                                     // reference's tetra loop reports hits on separated hulls through
                                     // isPointInSimplex's on-face branch (:1246-1256)
 #endif
-#ifndef GJKEPA_LDS_HULL_MIN
-#define GJKEPA_LDS_HULL_MIN 512     // tiers with G*K >= this read hull vertices from LDS, not registers
+// Per tier: hull vertices read from the group's LDS copy (1) instead of held in registers (0).
+// The LDS form frees 6K VGPRs per lane: EPA tier 0 then fits three waves per SIMD (168 VGPRs)
+// without spills (C2: EPA tier 0 6.10 -> 5.26 ms); GJK tier 0 is +1% either way.  Measured and
+// kept in registers: EPA tiers 1 / 2 at 3 waves (C2 tier 1 +8%, C5 tier 2 +15% slower: K = 4 support
+// sums read 24 LDS values per step), contact tier 1 at 2 waves (+14%).
+#ifndef GJKEPA_G0_LH
+#define GJKEPA_G0_LH 1
+#endif
+#ifndef GJKEPA_G1_LH
+#define GJKEPA_G1_LH 0
+#endif
+#ifndef GJKEPA_E0_LH
+#define GJKEPA_E0_LH 1
+#endif
+#ifndef GJKEPA_E1_LH
+#define GJKEPA_E1_LH 0
+#endif
+#ifndef GJKEPA_E2_LH
+#define GJKEPA_E2_LH 0
+#endif
+#ifndef GJKEPA_E3_LH
+#define GJKEPA_E3_LH 1             // 152 VGPRs: LDS-bound at 11 waves/CU (C4: EPA tier 3 100.4 -> 90.6 ms)
+#endif
+#ifndef GJKEPA_E4_LH
+#define GJKEPA_E4_LH 0
+#endif
+#ifndef GJKEPA_C0_LH
+#define GJKEPA_C0_LH 0
+#endif
+#ifndef GJKEPA_C1_LH
+#define GJKEPA_C1_LH 0
 #endif
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 5

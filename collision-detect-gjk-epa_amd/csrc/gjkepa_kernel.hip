@@ -84,9 +84,12 @@ enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
 // scratch, so a 16-pair GJK wave does not pay for polytope or contact arrays.
 template <typename T, typename TH, int G, int K, int VC_, int FC_> struct Lds {
     static constexpr int NH = G * K;
-    static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 ? G : 1;
+    // Coordinate columns are NH + 1 elements apart, so the six columns (hull A/B x, y, z) start on
+    // six different banks: the sphere test reads element i of all six at once (one lane each).
+    static constexpr int NHP = NH + GJKEPA_LDS_SKEW;
+    static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 && !GJKEPA_EPA_PLACE ? G : 1;
     static constexpr int NC = (VC_ == 0 && FC_ == 1) ? NH : 1;
-    TH hx[2][NH], hy[2][NH], hz[2][NH];  // hull A (0) / B (1) vertices, storage precision
+    TH hx[2][NHP], hy[2][NHP], hz[2][NHP];  // hull A (0) / B (1) vertices, storage precision
     union U {
         struct E {                       // EPA polytope (faces themselves are in registers)
             T vx[VC], vy[VC], vz[VC];    // vertices by id
@@ -109,14 +112,26 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_> struct Lds {
     } u;
 };
 
-template <typename T, typename TH, int G, int K, int VC, int FC> struct Ctx {
+// Byte distance between the LDS images of consecutive groups of a wave.  The images of the groups
+// that share a 32-lane half (the unit ds_read/ds_write banks over) are skewed by G dwords modulo
+// the 32 four-byte banks, so group g's lane l and group g+1's lane l, touching the same field, hit
+// different banks; an unpadded image size is often a multiple of 16 or 32 dwords, which puts every
+// group of a half on the same banks (GJK tier 0: 16 groups, 8 per half, two distinct bank offsets).
+template <typename L_t, int G> constexpr size_t lds_stride() {
+    size_t dw = (sizeof(L_t) + 7) / 8 * 2;                  // 8-byte aligned, in dwords
+    if (GJKEPA_LDS_SKEW && G < 32)
+        while (dw % 32 != (size_t)G) dw += 2;
+    return dw * 4;
+}
+
+template <typename T, typename TH, int G, int K, int VC, int FC, bool LH> struct Ctx {
     using L_t = Lds<T, TH, G, K, VC, FC>;
     L_t& L;
     Grp<G> g;
-    // Hull vertex k*G + gl of each hull: in registers, or (large-hull tiers, G*K >= GJKEPA_LDS_HULL_MIN)
-    // read from the group's LDS copy at each use, which frees 6K registers per lane so those
-    // tiers fit two waves per SIMD.  Same values either way (LDS holds the storage precision).
-    static constexpr bool kRegHull = G * K < GJKEPA_LDS_HULL_MIN;
+    // Hull vertex k*G + gl of each hull: in registers, or (LH: the tier's GJKEPA_*_LH) read from the
+    // group's LDS copy at each use, which frees 6K registers per lane so the tier fits one more wave
+    // per SIMD.  Same values either way (LDS holds the storage precision).
+    static constexpr bool kRegHull = !LH;
     T ax[kRegHull ? K : 1], ay[kRegHull ? K : 1], az[kRegHull ? K : 1];
     T bx[kRegHull ? K : 1], by[kRegHull ? K : 1], bz[kRegHull ? K : 1];
     int na, nb;
@@ -130,8 +145,8 @@ template <typename T, typename TH, int G, int K, int VC, int FC> struct Ctx {
     DEV V3<T> B(int i) const { return vmk<T>((T)L.hx[1][i], (T)L.hy[1][i], (T)L.hz[1][i]); }
     DEV V3<T> vert(int i) const { return vmk<T>(L.u.e.vx[i], L.u.e.vy[i], L.u.e.vz[i]); }
 };
-#define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC>
-#define CTX Ctx<T, TH, G, K, VC, FC>
+#define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC, bool LH>
+#define CTX Ctx<T, TH, G, K, VC, FC, LH>
 
 // ---------------------------------------------------------------- support mapping (:1030-1062)
 // indices: argmax_i d.a_i (first), argmax_j (-d).b_j (first); -dot(d,b) == dot(-d,b) bit for bit.
@@ -366,6 +381,44 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
     }
     __builtin_amdgcn_wave_barrier();
     GK_STAMP(SE_CMP);
+#if GJKEPA_EPA_PLACE
+    // New faces (horizon edge h coned to k) are built on the lane whose slot receives them, straight
+    // into its face registers.  Placement does not change results (the keys carry the order).  The
+    // visible faces' slots are freed first; each round, the group lanes that still have a free slot
+    // (lowest free row) take the next new faces in lane order, one per lane.  nf2 <= FC guarantees
+    // enough free slots in total, so the rounds end; usually one round places every new face.
+    const V3<T> P = c.vert(k);
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (vp[r] >= 0) F.fv[r] = kEmpty;
+    int top = 0;
+    for (int placed = 0; placed < nh;) {
+        int row = -1;
+#pragma unroll
+        for (int r = R - 1; r >= 0; --r)
+            if ((F.fv[r] & kEmpty) && r * G + gl < FC) row = r;
+        const uint64_t fl = c.g.ballot(row >= 0);
+        const int h = placed + mbcnt(fl);
+        if (row >= 0 && h < nh) {
+            const uint32_t uw = E.x.h.horu[h];
+            const int u = (int)(uw & 0xffu), w = (int)((uw >> 8) & 0xffu);
+            const V3<T> U = c.vert(u), W = c.vert(w);
+            const V3<T> n = uninml(U, W, P);
+            bad = bad || is_zero_nml(n);
+            const T dd = fabs(dot(vsub(zero3<T>(), U), n));
+            const uint32_t fv = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16), kk = E.x.h.hork[h];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r == row) { F.nx[r] = n.x; F.ny[r] = n.y; F.nz[r] = n.z; F.d[r] = dd; F.fv[r] = fv; F.key[r] = kk; }
+            const int sl = row * G + gl + 1;
+            top = top > sl ? top : sl;
+        }
+        placed += c.g.uni(popc(fl));
+    }
+    top = gmax<G>(top);
+    hw = hw > top ? hw : top;
+#else
     // New faces (horizon edge h coned to k) are built G at a time on group lane h % G and staged
     // in LDS, then copied into their slots.  Placement (results do not depend on it: the keys
     // carry the order): new face h takes the slot of visible face h, the ones beyond nvis are
@@ -430,6 +483,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         }
         __builtin_amdgcn_wave_barrier();
     }
+#endif
     GK_STAMP(SE_CONE);
     nf = nf2;
     if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
@@ -1507,13 +1561,13 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
 // simplex codes (5 words) in their own record slot and are routed to the smallest EPA tier that
 // holds their hulls.  Tier 0 takes every pair; hulls above its capacity are routed to tier 1.
 // WARM instantiations serve gjkepa_batch_warm_device (a.warm set); the plain ones carry no warm code.
-template <typename TIn, typename T, int G, int K, int MINW, bool WARM>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH, bool WARM>
 __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) {
     static_assert(G >= 4, "the tetrahedron faces run on quads");
     using L_t = Lds<T, TIn, G, K, 0, 0>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
-    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
@@ -1521,7 +1575,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SG_ROUTE);
-        Ctx<T, TIn, G, K, 0, 0> c{L, grp};
+        Ctx<T, TIn, G, K, 0, 0, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
         T o13[13];
@@ -1585,12 +1639,12 @@ DEV int contact_tier_for(int nmax) { return nmax <= GJKEPA_C0_G * GJKEPA_C0_K ? 
 // EPA kernel: the polytope loop for the pairs routed to this tier.  Depth, normal and the
 // diagnostics are parked in their final record fields and the pair goes to its contact tier.  A
 // polytope that outgrows the tier is routed to the next one (recomputed from the simplex codes).
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH>
 __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, VC, FC>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
-    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
@@ -1598,7 +1652,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
-        Ctx<T, TIn, G, K, VC, FC> c{L, grp};
+        Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
         c.nb = grp.uni(a.hull_cnt[hb]);
@@ -1687,20 +1741,21 @@ template <int SMALL> struct PairQueue {
 // EPA tier kernel with group refill: a group whose pair finished takes the next pair between
 // two EPA iterations (once at least REFILL groups of the wave are idle), so a wave no longer
 // runs every round to its slowest pair.  Results are the same as epa_kernel's.
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, int REFILL>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL>
 __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_args a) {
     constexpr int R = (FC + G - 1) / G;
     constexpr int NG = 64 / G;
     using L_t = Lds<T, TIn, G, K, VC, FC>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
-    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const int gid = grp.lane / G;
     const TIn* verts = (const TIn*)a.verts;
+    GK_STAMP_BEGIN();
     tally_begin();
     PairQueue<(2 * NG > 8 ? 2 * NG : 8)> q(a.route, a.n_pairs, a.route_code, a.ctr);
-    Ctx<T, TIn, G, K, VC, FC> c{L, grp};
+    Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
     EpaState<T, R> S;
     bool active = false;
     int64_t pair = 0;
@@ -1740,6 +1795,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             }
         }
         if (!__ballot(active || fresh)) break;
+        GK_STAMP(SE_ROUTE);
         if (fresh) {
             const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
             c.na = a.hull_cnt[ha];
@@ -1759,6 +1815,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             active = r == 0;
             if (!active) finish(r, T(0), zero3<T>());
         }
+        GK_STAMP(SE_LOAD);
         if (active) {
             T depth = 0;
             V3<T> n = zero3<T>();
@@ -1769,18 +1826,20 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
                 active = false;
             }
         }
+        GK_STAMP(SE_STORE);
     }
+    GK_STAMP_END();
     tally_end(a.tally);
 }
 
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
 // finished, from the depth and normal it parked; writes the final record.
-template <typename TIn, typename T, int G, int K, int MINW>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, 0, 1>;
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<G> grp;
-    L_t& L = *reinterpret_cast<L_t*>(smem + sizeof(L_t) * (grp.lane / G));
+    L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
@@ -1788,7 +1847,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
-        Ctx<T, TIn, G, K, 0, 1> c{L, grp};
+        Ctx<T, TIn, G, K, 0, 1, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
         c.nb = grp.uni(a.hull_cnt[hb]);
@@ -1835,11 +1894,11 @@ template <typename K_t> int grid_for(K_t kfn, size_t lds, int num_cus, int grid)
     return per_cu * num_cus;
 }
 
-template <typename TIn, typename T, int G, int K, int MINW>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
-    auto kfn = a.warm ? gk::gjk_kernel<TIn, T, G, K, MINW, true> : gk::gjk_kernel<TIn, T, G, K, MINW, false>;
+    auto kfn = a.warm ? gk::gjk_kernel<TIn, T, G, K, MINW, LH, true> : gk::gjk_kernel<TIn, T, G, K, MINW, LH, false>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 0, 0>) * GPW;
+    const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 0>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
     const int64_t chunks = (a.n_pairs + 63) / 64;
     if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
@@ -1847,14 +1906,14 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, int REFILL = 0>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL = 0>
 hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
     auto kfn = [] {
-        if constexpr (REFILL > 0) return gk::epa_kernel_refill<TIn, T, G, K, VC, FC, MINW, REFILL>;
-        else return gk::epa_kernel<TIn, T, G, K, VC, FC, MINW>;
+        if constexpr (REFILL > 0) return gk::epa_kernel_refill<TIn, T, G, K, VC, FC, MINW, LH, REFILL>;
+        else return gk::epa_kernel<TIn, T, G, K, VC, FC, MINW, LH>;
     }();
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, VC, FC>) * GPW;
+    const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, VC, FC>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
     const int64_t chunks = (a.n_pairs + 63) / 64;
     if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
@@ -1862,18 +1921,19 @@ hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-#define EPA_ARGS(t) GJKEPA_E##t##_G, GJKEPA_E##t##_K, GJKEPA_E##t##_VCAP, GJKEPA_E##t##_FCAP, GJKEPA_E##t##_MINW
+#define EPA_ARGS(t) GJKEPA_E##t##_G, GJKEPA_E##t##_K, GJKEPA_E##t##_VCAP, GJKEPA_E##t##_FCAP, GJKEPA_E##t##_MINW, \
+                    (GJKEPA_E##t##_LH != 0)
 
 template <typename TIn, typename T>
 hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
-    return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW>(a, s)
-                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW>(a, s);
+    return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW, (GJKEPA_G0_LH != 0)>(a, s)
+                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW, (GJKEPA_G1_LH != 0)>(a, s);
 }
-template <typename TIn, typename T, int G, int K, int MINW>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
-    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW>;
+    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH>;
     constexpr int GPW = 64 / G;
-    const size_t lds = sizeof(gk::Lds<T, TIn, G, K, 0, 1>) * GPW;
+    const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 1>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
     const int64_t chunks = (a.n_pairs + 63) / 64;
     if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
@@ -1882,8 +1942,8 @@ hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
 }
 template <typename TIn, typename T>
 hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
-    return tier == 0 ? launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW>(a, s)
-                     : launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW>(a, s);
+    return tier == 0 ? launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0)>(a, s)
+                     : launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0)>(a, s);
 }
 
 template <typename TIn, typename T>
