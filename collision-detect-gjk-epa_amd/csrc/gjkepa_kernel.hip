@@ -100,8 +100,10 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_> struct Lds {
                 struct H {                                                                 // hull_add lists
                     uint64_t visl[FC];                       // visible faces: ids | key << 32
                     uint32_t horu[FC], hork[FC];             // horizon edges: u | w << 8, new face key
+#if !GJKEPA_EPA_PLACE
                     T sn[GS][4];                             // new faces of one round: normal, |distance|
                     uint32_t sv[GS], sk[GS];                 //   ids, key
+#endif
                 } h;
                 struct S { T cur[FC]; T srt[FC]; } s;                                     // sorted_equal
                 struct O { uint32_t key[FC]; uint32_t ord[FC]; } o;                       // centroid order
@@ -1494,6 +1496,11 @@ DEV void tally_end(uint32_t* tally) {
     const int l = lane_id();
     if (l < GJKEPA_WS_TALLY && s_tally[l]) atomicAdd(&tally[l], s_tally[l]);
 }
+// A tier's tally is final when its kernel starts (pairs are only routed to later launches): a tier
+// nobody routed a pair to returns at once instead of scanning the route bytes.
+DEV bool tier_empty(const uint32_t* tally, int route_code) {
+    return route_code >= 0 && __builtin_amdgcn_readfirstlane(tally[route_code]) == 0;
+}
 DEV int pick_claim(const uint32_t* tally, int route_code, int64_t n_pairs, int claim) {
     if (route_code < 0 || claim <= 1) return claim;
     const uint32_t mine = __builtin_amdgcn_readfirstlane(tally[route_code]);
@@ -1571,6 +1578,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
+    if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
@@ -1648,6 +1656,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
+    if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
@@ -1753,6 +1762,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     const int gid = grp.lane / G;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
+    if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     PairQueue<(2 * NG > 8 ? 2 * NG : 8)> q(a.route, a.n_pairs, a.route_code, a.ctr);
     Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
@@ -1843,6 +1853,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
     GK_STAMP_BEGIN();
+    if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
@@ -1950,7 +1961,7 @@ template <typename TIn, typename T>
 hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
         case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
-        case 1: return launch_epa<TIn, T, EPA_ARGS(1)>(a, s);
+        case 1: return launch_epa<TIn, T, EPA_ARGS(1), GJKEPA_E1_REFILL>(a, s);
         case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL>(a, s);
         case 3: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
         default: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
