@@ -11,6 +11,10 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -55,6 +59,21 @@ struct DevBuf {
     }
 };
 
+struct HostBuf {                 // pinned host staging (one DMA each way for combined queries)
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 4096;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+
 struct DeviceState {
     std::mutex mu;
     bool init = false;
@@ -64,6 +83,8 @@ struct DeviceState {
     DevBuf h_foff, h_faces, h_nf, h_nv, h_st, h_hv, h_vi;   // gjkepa_hull_batch staging
     DevBuf b_pairs, b_count, b_ws;                          // gjkepa_broadphase staging
     DevBuf c_idx, c_hits, c_ws, c_n;                        // gjkepa_collide staging
+    DevBuf q_blk, q_ws;                                     // combined gjkepa_query batches
+    HostBuf q_host;
 };
 
 std::mutex g_table_mu;
@@ -282,6 +303,121 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Single-pair queries are combined across threads (the reference's `!$OMP PARALLEL DO ... CALL
+// GJKEPA` pattern): a caller queues its pair; if no batch is being run, it becomes the leader, takes
+// every queued pair with the same (version_, TOL_FF_), runs them as one gjkepa_batch and hands the
+// records back; otherwise it waits.  While one batch is on the GPU the other threads' pairs queue
+// up, so with T calling threads a round trip serves up to T pairs instead of one.
+struct Query {
+    int32_t version;
+    double tol_ff;
+    const double *p1, *p2;
+    int32_t n1, n2;
+    gjkepa_contact_f64 rec;
+    int rc = 0;
+    std::string err;             // gjkepa_last_error() of the batch, for the caller's thread
+    bool done = false;
+};
+struct Combiner {
+    std::mutex mu;
+    std::condition_variable cv, cv_lead;
+    std::vector<Query*> queue;
+    int inflight = 0;            // callers inside gjkepa_query
+    bool leader = false;
+};
+// A new leader waits up to this long for every caller inside gjkepa_query to queue its pair: the
+// callers the previous batch just answered come back within microseconds, and one round trip
+// costs far more than the wait.
+constexpr auto kGatherWait = std::chrono::microseconds(40);
+
+// GJKEPA_QUERY_STATS=1: batch count, mean batch size and mean round trip printed at exit (tuning aid)
+struct QueryStats {
+    std::atomic<int64_t> batches{0}, queries{0}, ns{0};
+    bool on = std::getenv("GJKEPA_QUERY_STATS") != nullptr;
+    ~QueryStats() {
+        if (on && batches > 0)
+            std::fprintf(stderr, "gjkepa_query: %lld batches, %.2f pairs/batch, %.1f us/batch\n", (long long)batches.load(),
+                         (double)queries / (double)batches, 1e-3 * (double)ns / (double)batches);
+    }
+} g_qstats;
+std::mutex g_comb_mu;
+std::vector<Combiner*> g_comb;
+
+Combiner* combiner(int device) {
+    std::lock_guard<std::mutex> g(g_comb_mu);
+    if ((int)g_comb.size() <= device) g_comb.resize((size_t)device + 1, nullptr);
+    if (!g_comb[(size_t)device]) g_comb[(size_t)device] = new Combiner();
+    return g_comb[(size_t)device];
+}
+
+// Run one batch of queued queries (all with the same version_ / TOL_FF_) on `device`.  The batch
+// is packed straight into pinned host memory as [records | vertices | offsets | counts | pairs],
+// copied to the device in one DMA, run, and its records copied back in one DMA.
+int run_queries_on(DeviceState* d, std::vector<Query*>& qs, int device) {
+    const size_t nq = qs.size();
+    size_t nv = 0;
+    for (Query* q : qs) nv += 3 * (size_t)(q->n1 + q->n2);
+    const size_t rec = sizeof(gjkepa_contact_f64);
+    const size_t o_v = nq * rec, o_off = o_v + 8 * (nv + 1), o_cnt = o_off + 8 * 2 * nq;
+    const size_t o_pr = o_cnt + 4 * 2 * nq, total = o_pr + 4 * 2 * nq;
+    std::lock_guard<std::mutex> g(d->mu);
+    int rc = init_device(d, device);
+    if (rc) return rc;
+    hipError_t e;
+    if ((e = d->q_host.ensure(total)) != hipSuccess || (e = d->q_blk.ensure(total)) != hipSuccess ||
+        (e = d->q_ws.ensure((size_t)gjkepa_workspace_bytes((int64_t)nq))) != hipSuccess)
+        return hip_fail(e, "query staging allocation");
+    char* h = (char*)d->q_host.p;
+    double* v = (double*)(h + o_v);
+    int64_t* off = (int64_t*)(h + o_off);
+    int32_t* cnt = (int32_t*)(h + o_cnt);
+    int32_t* pr = (int32_t*)(h + o_pr);
+    size_t o = 0;
+    for (size_t j = 0; j < nq; ++j) {
+        const Query* q = qs[j];
+        off[2 * j] = (int64_t)o;
+        cnt[2 * j] = q->n1;
+        std::memcpy(v + o, q->p1, sizeof(double) * 3 * (size_t)q->n1);
+        o += 3 * (size_t)q->n1;
+        off[2 * j + 1] = (int64_t)o;
+        cnt[2 * j + 1] = q->n2;
+        std::memcpy(v + o, q->p2, sizeof(double) * 3 * (size_t)q->n2);
+        o += 3 * (size_t)q->n2;
+        pr[2 * j] = (int32_t)(2 * j);
+        pr[2 * j + 1] = (int32_t)(2 * j + 1);
+    }
+    hipStream_t s = d->stream;
+    char* dv = (char*)d->q_blk.p;
+    if ((e = hipMemcpyAsync(dv + o_v, h + o_v, total - o_v, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    rc = enqueue(qs[0]->version, qs[0]->tol_ff, GJKEPA_DTYPE_F64, GJKEPA_PREC_F64, dv + o_v, (const int64_t*)(dv + o_off),
+                 (const int32_t*)(dv + o_cnt), (const int32_t*)(dv + o_pr), (int64_t)nq, dv, d->q_ws.p,
+                 (int64_t)d->q_ws.cap, s, d->num_cus);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(h, dv, o_v, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    for (size_t j = 0; j < nq; ++j) std::memcpy(&qs[j]->rec, h + j * rec, rec);
+    return 0;
+}
+
+void run_queries(std::vector<Query*>& qs, int device) {
+    int rc = 0;
+    DeviceState* d = device_state(device, &rc);
+    if (d) rc = run_queries_on(d, qs, device);
+    for (Query* q : qs) {
+        q->rc = rc;
+        if (rc) q->err = g_err;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
 int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, const double* p2, int32_t n2,
                  int8_t* collision, int32_t* colli_type, double* nearest_points, double* collision_normal,
                  double* collision_point, double* penetration_depth, int32_t* status, int32_t device) {
@@ -289,16 +425,45 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
         !penetration_depth)
         return fail(GJKEPA_E_ARG, "null pointer");
     if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
-    std::vector<double> pool((size_t)3 * (size_t)(n1 + n2) + 1, 0.0);
-    std::memcpy(pool.data(), p1, sizeof(double) * 3 * (size_t)n1);
-    std::memcpy(pool.data() + 3 * (size_t)n1, p2, sizeof(double) * 3 * (size_t)n2);
-    int64_t off[2] = {0, 3 * (int64_t)n1};
-    int32_t cnt[2] = {n1, n2};
-    int32_t pr[2] = {0, 1};
-    gjkepa_contact_f64 r;
-    int rc = gjkepa_batch(version, tol_ff, GJKEPA_DTYPE_F64, GJKEPA_PREC_F64, pool.data(), (int64_t)pool.size(),
-                          off, cnt, 2, pr, 1, &r, device);
-    if (rc) return rc;
+    int rc = 0;
+    if (!device_state(device, &rc)) return rc;
+    Combiner* cb = combiner(device);
+    Query me{version, tol_ff, p1, p2, n1, n2, {}};
+    {
+        std::unique_lock<std::mutex> lk(cb->mu);
+        cb->queue.push_back(&me);
+        ++cb->inflight;
+        cb->cv_lead.notify_one();
+        for (;;) {
+            cb->cv.wait(lk, [&] { return me.done || !cb->leader; });
+            if (me.done) break;
+            cb->leader = true;                           // lead one batch: the queued pairs like the first
+            const auto until = std::chrono::steady_clock::now() + kGatherWait;
+            while ((int)cb->queue.size() < cb->inflight &&
+                   cb->cv_lead.wait_until(lk, until) != std::cv_status::timeout) {
+            }
+            std::vector<Query*> batch, rest;
+            for (Query* q : cb->queue)
+                (q->version == cb->queue[0]->version && q->tol_ff == cb->queue[0]->tol_ff ? batch : rest).push_back(q);
+            cb->queue.swap(rest);
+            lk.unlock();
+            const auto t0 = std::chrono::steady_clock::now();
+            run_queries(batch, device);
+            if (g_qstats.on) {
+                g_qstats.batches += 1;
+                g_qstats.queries += (int64_t)batch.size();
+                g_qstats.ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+            }
+            lk.lock();
+            for (Query* q : batch) q->done = true;
+            cb->leader = false;
+            cb->cv.notify_all();
+        }
+        --cb->inflight;
+        rc = me.rc;
+    }
+    if (rc) return fail(rc, me.err);
+    const gjkepa_contact_f64& r = me.rec;
     *collision = r.collision;
     *colli_type = r.colli_type;
     // nearest_points_(2,3), Fortran column-major: (1,k) = p1, (2,k) = p2

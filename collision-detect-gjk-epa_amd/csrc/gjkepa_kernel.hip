@@ -1466,20 +1466,27 @@ DEV uint32_t match16(uint4 v, uint32_t code) {
 // Work units of a launch (guided chunking): 64-pair chunks first, then the last `tail` pairs in
 // units of SMALL pairs, so a wave that takes its last unit late holds a few pairs, not 64.  The
 // tail covers about 64 pairs per workgroup of the grid (at most half the pairs).
-template <int SMALL> struct Units {
+struct Units {
     int64_t n_pairs, nbig, nunits;
-    DEV explicit Units(int64_t n) : n_pairs(n) {
+    int small;
+    DEV Units(int64_t n, int small_) : n_pairs(n), small(small_) {
         int64_t tail = (int64_t)gridDim.x * 64;
         if (tail > n / 2) tail = n / 2;
         nbig = (n - tail) / 64;
-        nunits = nbig + (n - nbig * 64 + SMALL - 1) / SMALL;
+        nunits = nbig + (n - nbig * 64 + small - 1) / small;
     }
     DEV void range(int64_t u, int64_t& p0, int& len) const {
         if (u < nbig) { p0 = u * 64; len = 64; }
-        else { p0 = nbig * 64 + (u - nbig) * SMALL; len = SMALL; }
+        else { p0 = nbig * 64 + (u - nbig) * small; len = small; }
         if (p0 + len > n_pairs) len = (int)(n_pairs - p0);
     }
 };
+// Tail unit size: SMALL pairs, or one wave-round (64 / G pairs) when the launch has fewer than 8
+// pairs per workgroup (a latency-bound batch, e.g. combined single-pair queries: spread the pairs
+// over more waves instead of queueing them behind each other in one).
+template <int G, int SMALL> DEV int tail_unit(int64_t n) {
+    return n <= (int64_t)gridDim.x * 8 ? (64 / G < SMALL ? 64 / G : SMALL) : SMALL;
+}
 
 // Route tallies (workspace): each wave counts the pairs it routes per code in LDS and adds them to
 // the launch-wide tallies once at its end; a later launch reads its own code's tally to pick dense
@@ -1515,7 +1522,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
     const int64_t nchunks = (n_pairs + 63) / 64;
     uint32_t next = 0;
     if (claim <= 1 || route_code < 0) {
-        const Units<(64 / G > 8 ? 64 / G : 8)> U(n_pairs);
+        const Units U(n_pairs, tail_unit<G, (64 / G > 8 ? 64 / G : 8)>(n_pairs));
         if ((int64_t)blockIdx.x < U.nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
         int64_t u = blockIdx.x;
         while (u < U.nunits) {
@@ -1708,9 +1715,9 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
 
 // Wave-uniform queue of the pairs routed to a launch, one work unit at a time (first unit
 // static, later ones from the launch counter as in for_each_routed_pair).
-template <int SMALL> struct PairQueue {
+struct PairQueue {
     const uint8_t* route;
-    Units<SMALL> U;
+    Units U;
     int64_t ch, p0;
     uint32_t* ctr;
     uint32_t next;
@@ -1723,8 +1730,8 @@ template <int SMALL> struct PairQueue {
         const int64_t p = p0 + lane_id();
         m = __ballot(lane_id() < len && (int)route[p] == code);
     }
-    DEV PairQueue(const uint8_t* route_, int64_t n, int code_, uint32_t* ctr_)
-        : route(route_), U(n), ch(blockIdx.x), p0(0), ctr(ctr_), next(0), m(0), code(code_), done(false) {
+    DEV PairQueue(const uint8_t* route_, int64_t n, int small, int code_, uint32_t* ctr_)
+        : route(route_), U(n, small), ch(blockIdx.x), p0(0), ctr(ctr_), next(0), m(0), code(code_), done(false) {
         if (ch < U.nunits) {
             if (lane_id() == 0) next = gridDim.x + atomicAdd(ctr, 1u);
             load_chunk();
@@ -1764,7 +1771,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
-    PairQueue<(2 * NG > 8 ? 2 * NG : 8)> q(a.route, a.n_pairs, a.route_code, a.ctr);
+    PairQueue q(a.route, a.n_pairs, tail_unit<G, (2 * NG > 8 ? 2 * NG : 8)>(a.n_pairs), a.route_code, a.ctr);
     Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
     EpaState<T, R> S;
     bool active = false;
@@ -1898,6 +1905,13 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
 // ---------------------------------------------------------------- host-side launch table
 namespace {
 
+// no more workgroups than the launch has work units: 64-pair chunks, or one wave-round (64 / G
+// pairs) each for a small batch (the kernels' tail_unit)
+template <int G> int grid_cap(int64_t n_pairs, int grid) {
+    const int64_t chunks = (n_pairs + 63) / 64, rounds = (n_pairs + 64 / G - 1) / (64 / G);
+    const int64_t want = rounds <= (int64_t)grid * 8 / (64 / G) ? rounds : chunks;
+    return (int)(want < 1 ? 1 : want < grid ? want : grid);
+}
 template <typename K_t> int grid_for(K_t kfn, size_t lds, int num_cus, int grid) {
     if (grid > 0) return grid;
     int per_cu = 0;
@@ -1911,8 +1925,7 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 0>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
-    const int64_t chunks = (a.n_pairs + 63) / 64;
-    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    grid = grid_cap<G>(a.n_pairs, grid);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
@@ -1926,8 +1939,7 @@ hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, VC, FC>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
-    const int64_t chunks = (a.n_pairs + 63) / 64;
-    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    grid = grid_cap<G>(a.n_pairs, grid);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
@@ -1946,8 +1958,7 @@ hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 1>, G>() * GPW;
     int grid = grid_for(kfn, lds, a.num_cus, a.grid);
-    const int64_t chunks = (a.n_pairs + 63) / 64;
-    if (chunks < grid) grid = (int)(chunks > 0 ? chunks : 1);
+    grid = grid_cap<G>(a.n_pairs, grid);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
