@@ -18,4 +18,10 @@ echo "== bench C2 $(date)" && timeout -k 10 400 python bench.py > $OUT/bench_c2.
 echo "== rocprof C2 $(date)" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-f32-leg --no-warm-leg > $OUT/prof_bench.json 2> $OUT/prof.err && \
 echo "== pmc $(date)" && timeout -k 10 600 bash tools/pmc.sh $TAG > $OUT/pmc.log 2>&1 && cat $OUT/pmc.log && \
 echo "== call pattern $(date)" && OMP_NUM_THREADS=16 timeout -k 10 300 tests/fortran/build/bench_callpattern 100000 > $OUT/callpattern.txt 2>&1 && cat $OUT/callpattern.txt && \
-echo "== done $(date)"
+echo "== done $(date)" || exit 1
+if [ -n "$CFGS45" ]; then
+  for c in C4 C5; do
+    echo "== bench $c $(date)" && timeout -k 10 400 python bench.py --config $c > $OUT/bench_$(echo $c | tr C c).json 2> $OUT/bench_$c.err && cat $OUT/bench_$(echo $c | tr C c).json || exit 1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-f32-leg --no-warm-leg > $OUT/prof_$c.json 2> $OUT/prof_$c.err || exit 1
+  done
+fi
