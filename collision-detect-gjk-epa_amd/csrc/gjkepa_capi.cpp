@@ -109,6 +109,43 @@ int num_cus_current() {
     return cus;
 }
 
+// Second stream per device for the overlapped contact pass (GJKEPA_CONTACT_OVERLAP).  After EPA tier
+// 0 the chain forks: the contact pass for the pairs EPA tier 0 finished (most of the work) runs on an
+// internal stream, beside EPA tiers 1-4 on the caller's stream (a few long pairs: a small fraction
+// of the GPU for a long time); the branches join on the caller's stream.  Pairs tiers 1-4 finish
+// carry their own route codes (GJKEPA_ROUTE_CT0_LATE + tier) and get a contact pass of their own
+// after them, so the two streams never touch the same pair.  (A/B: the other way round, EPA tiers
+// 1-4 on a high-priority internal stream, was 2.5% slower on C2.)  Events and the stream are created once per device; the fork /
+// join enqueue is serialised per device so concurrent callers do not interleave their events.
+struct Fork {
+    std::mutex mu;
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_fork_mu;
+std::vector<Fork*> g_fork;
+
+int fork_state(Fork** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    std::lock_guard<std::mutex> g(g_fork_mu);
+    if ((int)g_fork.size() <= dev) g_fork.resize((size_t)dev + 1, nullptr);
+    Fork* f = g_fork[(size_t)dev];
+    if (!f) {
+        f = new Fork();
+        if ((e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming)) != hipSuccess) {
+            delete f;
+            return hip_fail(e, "overlap stream / events");
+        }
+        g_fork[(size_t)dev] = f;
+    }
+    *out = f;
+    return 0;
+}
+
 int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
             void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus, uint32_t* warm = nullptr) {
@@ -155,21 +192,45 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.tally = tally;
     a.out = out;
     a.num_cus = num_cus;
-    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {          // EPA tier t; polytope overflow -> t+1
+    auto epa_tier = [&](int t, hipStream_t es) -> int {  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
+        a.ct_base = (GJKEPA_CONTACT_OVERLAP && t > 0) ? GJKEPA_ROUTE_CT0_LATE : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
-        if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, s)) != hipSuccess) return hip_fail(e, "EPA tier launch");
+        hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, es);
+        return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");
+    };
+    auto contact_tiers = [&](int base, hipStream_t cs) -> int {   // contact features of EPA results
+        for (int t = 0; t < GJKEPA_CONTACT_TIERS; ++t) {
+            a.route_code = base + t;
+            a.next_code = -1;
+            a.ctr = ctr + launch++;
+            a.claim = (t == 0 && base == GJKEPA_ROUTE_CT0) ? 1 : kSparseClaim;
+            hipError_t er = gjkepa_launch_contact(t, vert_dtype, precision, a, cs);
+            if (er != hipSuccess) return hip_fail(er, "contact tier launch");
+        }
+        return 0;
+    };
+    int rc;
+    if ((rc = epa_tier(0, s))) return rc;
+    if (GJKEPA_CONTACT_OVERLAP) {
+        Fork* f = nullptr;
+        if ((rc = fork_state(&f))) return rc;
+        std::lock_guard<std::mutex> lk(f->mu);
+        if ((e = hipEventRecord(f->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2, f->fork, 0)) != hipSuccess)
+            return hip_fail(e, "contact pass fork");
+        if ((rc = contact_tiers(GJKEPA_ROUTE_CT0, f->s2))) return rc;
+        if ((e = hipEventRecord(f->join, f->s2)) != hipSuccess) return hip_fail(e, "contact pass join record");
+        for (int t = 1; t < GJKEPA_EPA_TIERS; ++t)
+            if ((rc = epa_tier(t, s))) return rc;
+        if ((rc = contact_tiers(GJKEPA_ROUTE_CT0_LATE, s))) return rc;
+        if ((e = hipStreamWaitEvent(s, f->join, 0)) != hipSuccess) return hip_fail(e, "contact pass join");
+        return 0;
     }
-    for (int t = 0; t < GJKEPA_CONTACT_TIERS; ++t) {      // contact features of every EPA result
-        a.route_code = GJKEPA_ROUTE_CT0 + t;
-        a.next_code = -1;
-        a.ctr = ctr + launch++;
-        a.claim = t == 0 ? 1 : kSparseClaim;
-        if ((e = gjkepa_launch_contact(t, vert_dtype, precision, a, s)) != hipSuccess) return hip_fail(e, "contact tier launch");
-    }
-    return 0;
+    for (int t = 1; t < GJKEPA_EPA_TIERS; ++t)
+        if ((rc = epa_tier(t, s))) return rc;
+    return contact_tiers(GJKEPA_ROUTE_CT0, s);
 }
 
 // select `device` and create its stream on first use (caller holds d->mu)

@@ -182,12 +182,15 @@
 #ifndef GJKEPA_C1_LH
 #define GJKEPA_C1_LH 0
 #endif
+#ifndef GJKEPA_CONTACT_OVERLAP
+#define GJKEPA_CONTACT_OVERLAP 1    // contact pass of EPA tier 0's pairs on a second stream, overlapping EPA tiers 1-4
+#endif
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 5
 #define GJKEPA_CONTACT_TIERS 2
 
 // workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair
-#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (9 launches used)
+#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (11 launches used)
 // then GJKEPA_WS_TALLY uint32 route tallies (indexed by route code): every kernel adds the pairs it
 // routes on; a launch whose own tally is at least 1/16 of the batch claims single chunks (dense),
 // otherwise runs of `claim` chunks (sparse scan)
@@ -196,7 +199,8 @@
 #define GJKEPA_ROUTE_DONE 0
 #define GJKEPA_ROUTE_GJK1 1
 #define GJKEPA_ROUTE_EPA0 0x10      // + EPA tier
-#define GJKEPA_ROUTE_CT0 0x20       // + contact tier
+#define GJKEPA_ROUTE_CT0 0x20       // + contact tier: pairs EPA tier 0 finished
+#define GJKEPA_ROUTE_CT0_LATE 0x22  // + contact tier: pairs EPA tiers 1-4 finished (GJKEPA_CONTACT_OVERLAP)
 
 struct gjkepa_gjk_args {
     const void* verts;
@@ -226,6 +230,7 @@ struct gjkepa_epa_args {
     uint8_t* route;
     int route_code;             // GJKEPA_ROUTE_EPA0 + tier
     int next_code;              // route code for polytope overflow; -1 on the last tier
+    int ct_base;                // route code base for the contact pass of the pairs this EPA tier finishes
     uint32_t* ctr;              // this launch's chunk counter (zero at launch)
     int claim;                  // 64-pair chunks taken per counter increment (sparse default)
     uint32_t* tally;            // pairs routed to each route code so far (GJKEPA_WS_TALLY entries)

@@ -1697,7 +1697,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
             T* rec = reinterpret_cast<T*>(slot);
             if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
             if (gl == 4) slot[sizeof(T) == 8 ? 27 : 14] = diag;
-            next = (uint8_t)(GJKEPA_ROUTE_CT0 + contact_tier_for(c.na > c.nb ? c.na : c.nb));
+            next = (uint8_t)(a.ct_base + contact_tier_for(c.na > c.nb ? c.na : c.nb));
         } else {                 // error status (last tier out of capacity: DEGENERATE): outputs zero, collision = 1
             T o13[13];
 #pragma unroll
@@ -1788,7 +1788,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             T* rec = reinterpret_cast<T*>(slot);
             if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
             if (gl == 4 % G) slot[sizeof(T) == 8 ? 27 : 14] = diag;
-            next = (uint8_t)(GJKEPA_ROUTE_CT0 + contact_tier_for(c.na > c.nb ? c.na : c.nb));
+            next = (uint8_t)(a.ct_base + contact_tier_for(c.na > c.nb ? c.na : c.nb));
         } else {
             T o13[13];
 #pragma unroll
