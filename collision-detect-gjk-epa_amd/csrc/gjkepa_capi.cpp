@@ -40,6 +40,10 @@ int hip_fail(hipError_t e, const char* what) {
 
 constexpr int64_t kWsHeader = 256;
 constexpr int kSparseClaim = 16;
+#ifndef GJKEPA_OVERLAP_MIN
+#define GJKEPA_OVERLAP_MIN (1 << 16)
+#endif
+constexpr int64_t kOverlapMin = GJKEPA_OVERLAP_MIN;   // batches from this size fork the contact pass (enqueue)
 #ifndef GJKEPA_DENSE_EPA_TIERS
 #define GJKEPA_DENSE_EPA_TIERS 2   // EPA tiers below this always claim single chunks; the others start
 #endif                             // sparse and switch to single chunks when their route tally is dense   // tiers that serve few pairs claim runs of 16 chunks (one 1-KB route load)
@@ -192,10 +196,13 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.tally = tally;
     a.out = out;
     a.num_cus = num_cus;
+    // small batches (e.g. combined single-pair queries) keep one stream: the fork's events and extra
+    // launches cost more latency than the overlap saves
+    const bool overlap = GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin;
     auto epa_tier = [&](int t, hipStream_t es) -> int {  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
-        a.ct_base = (GJKEPA_CONTACT_OVERLAP && t > 0) ? GJKEPA_ROUTE_CT0_LATE : GJKEPA_ROUTE_CT0;
+        a.ct_base = (overlap && t > 0) ? GJKEPA_ROUTE_CT0_LATE : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
         hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, es);
@@ -214,7 +221,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     };
     int rc;
     if ((rc = epa_tier(0, s))) return rc;
-    if (GJKEPA_CONTACT_OVERLAP) {
+    if (overlap) {
         Fork* f = nullptr;
         if ((rc = fork_state(&f))) return rc;
         std::lock_guard<std::mutex> lk(f->mu);
