@@ -113,18 +113,19 @@ int num_cus_current() {
     return cus;
 }
 
-// Second stream per device for the overlapped contact pass (GJKEPA_CONTACT_OVERLAP).  After EPA tier
-// 0 the chain forks: the contact pass for the pairs EPA tier 0 finished (most of the work) runs on an
-// internal stream, beside EPA tiers 1-4 on the caller's stream (a few long pairs: a small fraction
-// of the GPU for a long time); the branches join on the caller's stream.  Pairs tiers 1-4 finish
-// carry their own route codes (GJKEPA_ROUTE_CT0_LATE + tier) and get a contact pass of their own
-// after them, so the two streams never touch the same pair.  (A/B: the other way round, EPA tiers
-// 1-4 on a high-priority internal stream, was 2.5% slower on C2.)  Events and the stream are created once per device; the fork /
-// join enqueue is serialised per device so concurrent callers do not interleave their events.
+// Second stream per device for the overlapped contact passes (GJKEPA_CONTACT_OVERLAP).  The pairs
+// EPA tier t finishes carry the route codes GJKEPA_ROUTE_CT(t) + contact tier, and their contact pass
+// is forked onto an internal stream as soon as tier t is done, so it runs beside EPA tiers t+1..4:
+// on C2 the contact pass of EPA tier 0 (most of the hits) overlaps tier 1 (a few long pairs), on C5
+// that of tier 2 overlaps tier 3.  Every fork joins back into the caller's stream at the end of the
+// chain; the two streams never touch the same pair.  Events and the stream are created once per
+// device, and the enqueue is serialised per device so concurrent callers do not interleave their
+// events.  (A/B: the other way round, later EPA tiers on a high-priority internal stream beside the
+// contact pass, was 2.5% slower on C2.)
 struct Fork {
     std::mutex mu;
     hipStream_t s2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join = nullptr;
 };
 std::mutex g_fork_mu;
 std::vector<Fork*> g_fork;
@@ -138,9 +139,11 @@ int fork_state(Fork** out) {
     Fork* f = g_fork[(size_t)dev];
     if (!f) {
         f = new Fork();
-        if ((e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming)) != hipSuccess) {
+        e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking);
+        for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t)
+            e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming);
+        if (e != hipSuccess) {
             delete f;
             return hip_fail(e, "overlap stream / events");
         }
@@ -149,6 +152,21 @@ int fork_state(Fork** out) {
     *out = f;
     return 0;
 }
+
+// hull capacity (vertices) of EPA tier t (gjkepa_kernel.hip: epa_hull_cap)
+constexpr int epa_hull_cap(int t) {
+    return t == 0 ? GJKEPA_E0_G * GJKEPA_E0_K : t == 1 ? GJKEPA_E1_G * GJKEPA_E1_K : t == 2 ? GJKEPA_E2_G * GJKEPA_E2_K
+         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : GJKEPA_E4_G * GJKEPA_E4_K;
+}
+
+// launches of an overlapped chain: 2 GJK + the EPA tiers + each EPA tier's contact pass; every
+// launch owns one workspace counter
+constexpr int overlap_launches() {
+    int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS;
+    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) n += epa_hull_cap(t) <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
+    return n;
+}
+static_assert(overlap_launches() <= GJKEPA_WS_COUNTERS, "workspace launch counters");
 
 int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
@@ -199,45 +217,47 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     // small batches (e.g. combined single-pair queries) keep one stream: the fork's events and extra
     // launches cost more latency than the overlap saves
     const bool overlap = GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin;
-    auto epa_tier = [&](int t, hipStream_t es) -> int {  // EPA tier t; polytope overflow -> t+1
+    auto epa_tier = [&](int t) -> int {                  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
-        a.ct_base = (overlap && t > 0) ? GJKEPA_ROUTE_CT0_LATE : GJKEPA_ROUTE_CT0;
+        a.ct_base = overlap ? GJKEPA_ROUTE_CT(t) : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
-        hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, es);
+        hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, s);
         return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");
     };
-    auto contact_tiers = [&](int base, hipStream_t cs) -> int {   // contact features of EPA results
-        for (int t = 0; t < GJKEPA_CONTACT_TIERS; ++t) {
+    // contact features of the EPA results under route codes base + contact tier (tiers 0..ntiers-1)
+    auto contact_tiers = [&](int base, int ntiers, hipStream_t cs) -> int {
+        for (int t = 0; t < ntiers; ++t) {
             a.route_code = base + t;
             a.next_code = -1;
             a.ctr = ctr + launch++;
-            a.claim = (t == 0 && base == GJKEPA_ROUTE_CT0) ? 1 : kSparseClaim;
+            a.claim = (t == 0 && base <= GJKEPA_ROUTE_CT(0)) ? 1 : kSparseClaim;
             hipError_t er = gjkepa_launch_contact(t, vert_dtype, precision, a, cs);
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
         }
         return 0;
     };
     int rc;
-    if ((rc = epa_tier(0, s))) return rc;
     if (overlap) {
         Fork* f = nullptr;
         if ((rc = fork_state(&f))) return rc;
         std::lock_guard<std::mutex> lk(f->mu);
-        if ((e = hipEventRecord(f->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2, f->fork, 0)) != hipSuccess)
-            return hip_fail(e, "contact pass fork");
-        if ((rc = contact_tiers(GJKEPA_ROUTE_CT0, f->s2))) return rc;
-        if ((e = hipEventRecord(f->join, f->s2)) != hipSuccess) return hip_fail(e, "contact pass join record");
-        for (int t = 1; t < GJKEPA_EPA_TIERS; ++t)
-            if ((rc = epa_tier(t, s))) return rc;
-        if ((rc = contact_tiers(GJKEPA_ROUTE_CT0_LATE, s))) return rc;
-        if ((e = hipStreamWaitEvent(s, f->join, 0)) != hipSuccess) return hip_fail(e, "contact pass join");
+        for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
+            if ((rc = epa_tier(t))) return rc;
+            if ((e = hipEventRecord(f->fork[t], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2, f->fork[t], 0)) != hipSuccess)
+                return hip_fail(e, "contact pass fork");
+            // an EPA tier whose hulls all fit contact tier 0 produces no contact-tier-1 pairs
+            const int nct = epa_hull_cap(t) <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
+            if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), nct, f->s2))) return rc;
+        }
+        if ((e = hipEventRecord(f->join, f->s2)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join, 0)) != hipSuccess)
+            return hip_fail(e, "contact pass join");
         return 0;
     }
-    for (int t = 1; t < GJKEPA_EPA_TIERS; ++t)
-        if ((rc = epa_tier(t, s))) return rc;
-    return contact_tiers(GJKEPA_ROUTE_CT0, s);
+    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
+        if ((rc = epa_tier(t))) return rc;
+    return contact_tiers(GJKEPA_ROUTE_CT0, GJKEPA_CONTACT_TIERS, s);
 }
 
 // select `device` and create its stream on first use (caller holds d->mu)

@@ -183,14 +183,14 @@
 #define GJKEPA_C1_LH 0
 #endif
 #ifndef GJKEPA_CONTACT_OVERLAP
-#define GJKEPA_CONTACT_OVERLAP 1    // contact pass of EPA tier 0's pairs on a second stream, overlapping EPA tiers 1-4
+#define GJKEPA_CONTACT_OVERLAP 1    // each EPA tier's contact pass on a second stream, overlapping the later EPA tiers
 #endif
 #define GJKEPA_GJK_TIERS 2
 #define GJKEPA_EPA_TIERS 5
 #define GJKEPA_CONTACT_TIERS 2
 
 // workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair
-#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (11 launches used)
+#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (at most 15 launches used)
 // then GJKEPA_WS_TALLY uint32 route tallies (indexed by route code): every kernel adds the pairs it
 // routes on; a launch whose own tally is at least 1/16 of the batch claims single chunks (dense),
 // otherwise runs of `claim` chunks (sparse scan)
@@ -199,8 +199,9 @@
 #define GJKEPA_ROUTE_DONE 0
 #define GJKEPA_ROUTE_GJK1 1
 #define GJKEPA_ROUTE_EPA0 0x10      // + EPA tier
-#define GJKEPA_ROUTE_CT0 0x20       // + contact tier: pairs EPA tier 0 finished
-#define GJKEPA_ROUTE_CT0_LATE 0x22  // + contact tier: pairs EPA tiers 1-4 finished (GJKEPA_CONTACT_OVERLAP)
+#define GJKEPA_ROUTE_CT0 0x20       // + contact tier
+// with GJKEPA_CONTACT_OVERLAP, the pairs EPA tier t finishes go to contact tier c under code CT(t) + c
+#define GJKEPA_ROUTE_CT(t) (GJKEPA_ROUTE_CT0 + 2 * (t))
 
 struct gjkepa_gjk_args {
     const void* verts;
