@@ -3,9 +3,10 @@
 // Host-buffer entries (gjkepa_query, gjkepa_batch) own per-device staging buffers that grow as
 // needed and are reused; they are serialised per device by a mutex, so concurrent callers (the
 // reference's `!$OMP PARALLEL DO ... CALL GJKEPA` pattern) are safe.  gjkepa_batch_device never
-// allocates or synchronises: it enqueues a 256-byte counter / tally reset and nine kernels (2 GJK +
-// 5 EPA + 2 contact tiers); each kernel takes 64-pair chunks (or runs of 16) from its own counter.  gjkepa_hull_batch(_device)
-// follow the same pattern for the batched convex-hull kernels (two tiers over one cloud list).
+// allocates or synchronises: it enqueues a 256-byte counter / tally reset and the tier kernels (2 GJK +
+// 5 EPA tiers, and the contact passes, forked onto a second stream for large batches); each kernel
+// takes 64-pair chunks (or runs of 16) from its own counter.  gjkepa_hull_batch(_device) follow the
+// same pattern for the batched convex-hull kernels (two tiers over one cloud list).
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
