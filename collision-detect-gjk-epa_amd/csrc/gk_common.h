@@ -9,6 +9,10 @@
 #include <cmath>
 #include <cstdint>
 
+#ifndef GJKEPA_FMAX_REDUCE
+#define GJKEPA_FMAX_REDUCE 1
+#endif
+
 namespace gk {
 
 #define DEV __device__ __forceinline__
@@ -147,10 +151,22 @@ template <int S, int N, typename T> DEV void argmin_steps(T& v, int& i) {
         argmin_steps<S + 1, N>(v, i);
     }
 }
+// Value-only max / min reductions.  Floating values take v_max_f64 / v_min_f64 (one instruction a
+// step instead of compare + two selects): the callers only compare against the result or use values
+// that cannot be -0 (squared norms, |distances|), and a NaN operand never wins — as in the
+// reference's sequential `IF (t > mx)` scans.  (GJKEPA_FMAX_REDUCE=0: the select form, for A/B.)
+template <typename T> DEV T red_max(T a, T b) {
+    if constexpr (GJKEPA_FMAX_REDUCE && (sizeof(T) == 8 || sizeof(T) == 4) && T(0.5) != T(0)) return __builtin_fmax(a, b);
+    else return a > b ? a : b;
+}
+template <typename T> DEV T red_min(T a, T b) {
+    if constexpr (GJKEPA_FMAX_REDUCE && (sizeof(T) == 8 || sizeof(T) == 4) && T(0.5) != T(0)) return __builtin_fmin(a, b);
+    else return a < b ? a : b;
+}
 template <int S, int N, typename T> DEV void max_steps(T& v) {
     if constexpr (S < N) {
         T ov = xchg<S>(v);
-        v = ov > v ? ov : v;
+        v = red_max(ov, v);
         max_steps<S + 1, N>(v);
     }
 }
@@ -171,7 +187,7 @@ template <int G, typename T> DEV T gmax(T v) { max_steps<0, Grp<G>::kSteps>(v); 
 template <int S, int N, typename T> DEV void min_steps(T& v) {
     if constexpr (S < N) {
         T ov = xchg<S>(v);
-        v = ov < v ? ov : v;
+        v = red_min(ov, v);
         min_steps<S + 1, N>(v);
     }
 }
