@@ -25,3 +25,9 @@ if [ -n "$CFGS45" ]; then
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-f32-leg --no-warm-leg > $OUT/prof_$c.json 2> $OUT/prof_$c.err || exit 1
   done
 fi
+if [ -n "$PMC5" ]; then
+  echo "== pmc C5 $(date)" && timeout -k 10 600 bash tools/pmc.sh ${TAG}_c5 --config C5 > $OUT/pmc_c5.log 2>&1 || exit 1
+fi
+if [ -n "$GLOO2" ]; then
+  echo "== 2-rank gloo rehearsal $(date)" && timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --backend gloo --steps 3 --warmup 1 --pairs-per-gpu 262144 > $OUT/bench_2rank_gloo.json 2> $OUT/bench_2rank_gloo.err && cat $OUT/bench_2rank_gloo.json || exit 1
+fi
