@@ -45,6 +45,10 @@ constexpr int kSparseClaim = 16;
 #define GJKEPA_OVERLAP_MIN (1 << 16)
 #endif
 constexpr int64_t kOverlapMin = GJKEPA_OVERLAP_MIN;   // batches from this size fork the contact pass (enqueue)
+#ifndef GJKEPA_FUSED_MAX
+#define GJKEPA_FUSED_MAX 64
+#endif
+constexpr int64_t kFusedMax = GJKEPA_FUSED_MAX;       // batches up to this size run the one-kernel query path
 #ifndef GJKEPA_DENSE_EPA_TIERS
 #define GJKEPA_DENSE_EPA_TIERS 2   // EPA tiers below this always claim single chunks; the others start
 #endif                             // sparse and switch to single chunks when their route tally is dense   // tiers that serve few pairs claim runs of 16 chunks (one 1-KB route load)
@@ -179,6 +183,20 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     uint32_t* ctr = (uint32_t*)workspace;
     uint8_t* route = (uint8_t*)workspace + kWsHeader;
     hipError_t e;
+    if (!warm && n_pairs <= kFusedMax) {                 // small batch: one launch, one wave per pair
+        gjkepa_epa_args q{};
+        q.version = version;
+        q.tol_ff = tol_ff;
+        q.verts = verts;
+        q.hull_off = hull_off;
+        q.hull_cnt = hull_cnt;
+        q.pairs = pairs;
+        q.n_pairs = n_pairs;
+        q.out = out;
+        q.num_cus = num_cus;
+        if ((e = gjkepa_launch_query(vert_dtype, precision, q, s)) != hipSuccess) return hip_fail(e, "query kernel launch");
+        return 0;
+    }
     static_assert(sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY) <= kWsHeader, "workspace header");
     if ((e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY), s)) != hipSuccess)
         return hip_fail(e, "workspace counter reset");

@@ -244,3 +244,5 @@ hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjke
 hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
 // contact tiers take the same argument block (route_code = GJKEPA_ROUTE_CT0 + tier; next_code unused)
 hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
+// one-kernel path for small batches: one wave per pair (grid = n_pairs), GJK + EPA + contact features
+hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);

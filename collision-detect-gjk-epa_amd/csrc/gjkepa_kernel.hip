@@ -82,13 +82,14 @@ enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
 // Sized for the kernel that uses it: VC > 0 is the EPA polytope (VC vertices, FC face slots);
 // VC == 0 is the GJK kernel (FC == 0) or the contact kernel (FC == 1), which carry only their own
 // scratch, so a 16-pair GJK wave does not pay for polytope or contact arrays.
-template <typename T, typename TH, int G, int K, int VC_, int FC_> struct Lds {
+// FUSED: the one-kernel query path (query_kernel) keeps the contact arrays beside the polytope.
+template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = false> struct Lds {
     static constexpr int NH = G * K;
     // Coordinate columns are NH + 1 elements apart, so the six columns (hull A/B x, y, z) start on
     // six different banks: the sphere test reads element i of all six at once (one lane each).
     static constexpr int NHP = NH + GJKEPA_LDS_SKEW;
     static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 && !GJKEPA_EPA_PLACE ? G : 1;
-    static constexpr int NC = (VC_ == 0 && FC_ == 1) ? NH : 1;
+    static constexpr int NC = ((VC_ == 0 && FC_ == 1) || FUSED) ? NH : 1;
     TH hx[2][NHP], hy[2][NHP], hz[2][NHP];  // hull A (0) / B (1) vertices, storage precision
     union U {
         struct E {                       // EPA polytope (faces themselves are in registers)
@@ -126,11 +127,12 @@ template <typename L_t, int G> constexpr size_t lds_stride() {
     return dw * 4;
 }
 
-template <typename T, typename TH, int G, int K, int VC, int FC, bool LH> struct Ctx {
-    using L_t = Lds<T, TH, G, K, VC, FC>;
+template <typename T, typename TH, int G, int K, int VC, int FC, int LH> struct Ctx {
+    using L_t = Lds<T, TH, G, K, VC, FC, (LH == 2)>;
     L_t& L;
     Grp<G> g;
-    // Hull vertex k*G + gl of each hull: in registers, or (LH: the tier's GJKEPA_*_LH) read from the
+    // Hull vertex k*G + gl of each hull: in registers, or (LH 1: the tier's GJKEPA_*_LH; 2: the fused
+    // query kernel, whose LDS image also holds the contact arrays) read from the
     // group's LDS copy at each use, which frees 6K registers per lane so the tier fits one more wave
     // per SIMD.  Same values either way (LDS holds the storage precision).
     static constexpr bool kRegHull = !LH;
@@ -147,7 +149,7 @@ template <typename T, typename TH, int G, int K, int VC, int FC, bool LH> struct
     DEV V3<T> B(int i) const { return vmk<T>((T)L.hx[1][i], (T)L.hy[1][i], (T)L.hz[1][i]); }
     DEV V3<T> vert(int i) const { return vmk<T>(L.u.e.vx[i], L.u.e.vy[i], L.u.e.vz[i]); }
 };
-#define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC, bool LH>
+#define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC, int LH>
 #define CTX Ctx<T, TH, G, K, VC, FC, LH>
 
 // ---------------------------------------------------------------- support mapping (:1030-1062)
@@ -1849,6 +1851,71 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     tally_end(a.tally);
 }
 
+// One-kernel query path for small batches (combined single-pair queries, gjkepa_query): one wave per
+// pair runs the sphere test, GJK, EPA and the contact features back to back with the largest tier's
+// capacities (64 lanes, hulls up to 256 vertices, EPA tier 4's polytope: never defers), so a batch
+// costs one launch instead of the tier chain's ten.  Same device functions as the tier kernels, so
+// the records are the chain's bit for bit.
+template <typename TIn, typename T>
+__global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
+    constexpr int G = 64, K = GJKEPA_MAX_HULL_VERTS / 64, VC = GJKEPA_E4_VCAP, FC = GJKEPA_E4_FCAP;
+    using L_t = Lds<T, TIn, G, K, VC, FC, true>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    L_t& L = *reinterpret_cast<L_t*>(smem);
+    const Grp<G> grp;
+    const int gl = grp.gl;
+    const int64_t pair = blockIdx.x;
+    if (pair >= a.n_pairs) return;
+    const TIn* verts = (const TIn*)a.verts;
+    Ctx<T, TIn, G, K, VC, FC, 2> c{L, grp};
+    const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+    const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
+    T o13[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) o13[i] = T(0);
+    if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
+        store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+        return;
+    }
+    c.na = na;
+    c.nb = nb;
+    if (load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb])) {
+        store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+        return;
+    }
+    uint32_t kc[4];
+    int gjk_it = 0;
+    int r = gjk_phase(c, kc, gjk_it, GJKEPA_AXIS_REJECT != 0);
+    __builtin_amdgcn_wave_barrier();
+    if (r == PH_MISS) {
+        store_record<G, T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
+        return;
+    }
+    if (r != PH_HIT) {                                   // GJK-phase error (reference would STOP)
+        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
+        return;
+    }
+    T depth;
+    V3<T> n;
+    uint32_t de = 0;
+    r = epa_phase(c, kc, depth, n, de);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t diag = ((uint32_t)gjk_it & 0xffu) | de;
+    if (r != 0) {                                        // last tier out of capacity: DEGENERATE
+        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
+        return;
+    }
+    r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
+    __builtin_amdgcn_wave_barrier();
+    if (r < 0) {
+        store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 13; ++i) o13[i] = T(0);
+        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, diag);
+    }
+}
+
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
 // finished, from the depth and normal it parked; writes the final record.
 template <typename TIn, typename T, int G, int K, int MINW, bool LH>
@@ -1992,6 +2059,18 @@ extern "C" int gjkepa_diag_stamps(unsigned long long* out, int reset) {
     return gk::kStamps;
 }
 #endif
+
+template <typename TIn, typename T> hipError_t launch_query(const gjkepa_epa_args& a, hipStream_t s) {
+    using L_t = gk::Lds<T, TIn, 64, GJKEPA_MAX_HULL_VERTS / 64, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, true>;
+    auto kfn = gk::query_kernel<TIn, T>;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)a.n_pairs), dim3(64), sizeof(L_t), s, a);
+    return hipGetLastError();
+}
+hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
+    if (vert_dtype == GJKEPA_DTYPE_F32)
+        return precision == GJKEPA_PREC_F64 ? launch_query<float, double>(a, s) : launch_query<float, float>(a, s);
+    return precision == GJKEPA_PREC_F64 ? launch_query<double, double>(a, s) : launch_query<double, float>(a, s);
+}
 
 hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s) {
     if (vert_dtype == GJKEPA_DTYPE_F32)
