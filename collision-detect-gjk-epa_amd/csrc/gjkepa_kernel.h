@@ -161,9 +161,6 @@
 #ifndef GJKEPA_G1_LH
 #define GJKEPA_G1_LH 0
 #endif
-#ifndef GJKEPA_EPA_PREFETCH
-#define GJKEPA_EPA_PREFETCH 0    // refill kernels pop each group's next pair one refill ahead (A/B)
-#endif
 #ifndef GJKEPA_E0_LH
 #define GJKEPA_E0_LH 1
 #endif

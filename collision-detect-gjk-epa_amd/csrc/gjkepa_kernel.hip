@@ -1799,72 +1799,31 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
         }
         if (gl == 0) { a.route[pair] = next; tally_route(next); }
     };
-    // PF: each group holds its next pair, popped one refill ahead; its hull indices are loaded at
-    // that refill and its hull counts / offsets after the next EPA step, so a fresh pair's refill
-    // waits on one level of global loads (slot + vertices) instead of three.
-    constexpr bool PF = GJKEPA_EPA_PREFETCH != 0;
-    int64_t pf = -1;
-    int32_t pf_ha = 0, pf_hb = 0, pf_na = 0, pf_nb = 0;
-    int64_t pf_oa = 0, pf_ob = 0;
-    bool pf_meta = false;
     for (;;) {
         // refill idle groups (in group order) once enough of them are idle
         const uint64_t idle = __ballot(gl == 0 && !active);
         const int nidle = popc(idle);
-        bool fresh = false, fresh_pf = false, pf_new = false;
-        if constexpr (PF) {
-            if ((!q.done || __ballot(pf >= 0)) && (nidle >= REFILL || nidle == NG)) {
-                if (!active && pf >= 0) { pair = pf; fresh = fresh_pf = true; pf = -1; }
-                const uint64_t need = __ballot(gl == 0 && !active && !fresh);
-                const uint64_t want = __ballot(gl == 0 && pf < 0);
+        bool fresh = false;
+        if (!q.done && (nidle >= REFILL || nidle == NG)) {
 #pragma unroll
-                for (int g = 0; g < NG; ++g) {
-                    if ((need >> (g * G)) & 1ull) {
-                        const int64_t p = q.pop();
-                        if (p >= 0 && gid == g) { pair = p; fresh = true; }
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < NG; ++g) {
-                    if ((want >> (g * G)) & 1ull) {
-                        const int64_t p = q.pop();
-                        if (gid == g) pf = p;
-                    }
-                }
-                pf_new = pf >= 0 && ((want >> (gid * G)) & 1ull);
-            }
-        } else {
-            if (!q.done && (nidle >= REFILL || nidle == NG)) {
-#pragma unroll
-                for (int g = 0; g < NG; ++g) {
-                    if ((idle >> (g * G)) & 1ull) {
-                        const int64_t p = q.pop();
-                        if (p >= 0 && gid == g) { pair = p; fresh = true; }
-                    }
+            for (int g = 0; g < NG; ++g) {
+                if ((idle >> (g * G)) & 1ull) {
+                    const int64_t p = q.pop();
+                    if (p >= 0 && gid == g) { pair = p; fresh = true; }
                 }
             }
         }
         if (!__ballot(active || fresh)) break;
         GK_STAMP(SE_ROUTE);
         if (fresh) {
-            int64_t oa, ob;
-            if (PF && fresh_pf) {
-                if (!pf_meta) {
-                    pf_na = a.hull_cnt[pf_ha]; pf_nb = a.hull_cnt[pf_hb];
-                    pf_oa = a.hull_off[pf_ha]; pf_ob = a.hull_off[pf_hb];
-                }
-                c.na = pf_na; c.nb = pf_nb; oa = pf_oa; ob = pf_ob;
-            } else {
-                const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
-                c.na = a.hull_cnt[ha];
-                c.nb = a.hull_cnt[hb];
-                oa = a.hull_off[ha]; ob = a.hull_off[hb];
-            }
+            const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+            c.na = a.hull_cnt[ha];
+            c.nb = a.hull_cnt[hb];
             const uint32_t* slot = reinterpret_cast<const uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
             uint32_t kc[4];
             kc[0] = slot[0]; kc[1] = slot[1]; kc[2] = slot[2]; kc[3] = slot[3];
             gjk_it = slot[4];
-            load_hulls(c, verts + oa, verts + ob);
+            load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
             S.iters = 1; S.nf = 0;
             int r = ST_DEFER;
             if (c.na <= G * K && c.nb <= G * K) {
@@ -1875,8 +1834,6 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             active = r == 0;
             if (!active) finish(r, T(0), zero3<T>());
         }
-        // only now, with a taken pair's metadata read, may the new prefetch's hull indices replace it
-        if (PF && pf_new) { pf_ha = a.pairs[2 * pf]; pf_hb = a.pairs[2 * pf + 1]; pf_meta = false; }
         GK_STAMP(SE_LOAD);
         if (active) {
             T depth = 0;
@@ -1886,13 +1843,6 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             if (r != ST_CONT) {
                 finish(r, depth, n);
                 active = false;
-            }
-        }
-        if constexpr (PF) {
-            if (pf >= 0 && !pf_meta) {
-                pf_na = a.hull_cnt[pf_ha]; pf_nb = a.hull_cnt[pf_hb];
-                pf_oa = a.hull_off[pf_ha]; pf_ob = a.hull_off[pf_hb];
-                pf_meta = true;
             }
         }
         GK_STAMP(SE_STORE);
