@@ -118,42 +118,51 @@ int num_cus_current() {
     return cus;
 }
 
-// Second stream per device for the overlapped contact passes (GJKEPA_CONTACT_OVERLAP).  The pairs
-// EPA tier t finishes carry the route codes GJKEPA_ROUTE_CT(t) + contact tier, and their contact pass
-// is forked onto an internal stream as soon as tier t is done, so it runs beside EPA tiers t+1..4:
-// on C2 the contact pass of EPA tier 0 (most of the hits) overlaps tier 1 (a few long pairs), on C5
-// that of tier 2 overlaps tier 3.  Every fork joins back into the caller's stream at the end of the
-// chain; the two streams never touch the same pair.  Events and the stream are created once per
-// device, and the enqueue is serialised per device so concurrent callers do not interleave their
-// events.  (A/B: the other way round, later EPA tiers on a high-priority internal stream beside the
-// contact pass, was 2.5% slower on C2.)
+// Second stream for the overlapped contact passes (GJKEPA_CONTACT_OVERLAP).  The pairs EPA tier t
+// finishes carry the route codes GJKEPA_ROUTE_CT(t) + contact tier, and their contact pass is forked
+// onto an internal stream as soon as tier t is done, so it runs beside EPA tiers t+1..4: on C2 the
+// contact pass of EPA tier 0 (most of the hits) overlaps tier 1 (a few long pairs), on C5 that of
+// tier 2 overlaps tier 3.  Every fork joins back into the caller's stream at the end of the chain;
+// the two streams never touch the same pair.  The internal stream and its events belong to one
+// (device, caller stream): callers on different streams never share them, so one caller's work
+// never waits on another's contact passes, and an internal stream that joins a caller's graph
+// capture (the fork / join events make it part of the capture) carries only that caller's work.
+// Up to kForkMax caller streams get their own; further streams run the chain on one stream.
+// (A/B: the other way round, later EPA tiers on a high-priority internal stream beside the contact
+// pass, was 2.5% slower on C2.)
 struct Fork {
     std::mutex mu;
     hipStream_t s2 = nullptr;
     hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join = nullptr;
 };
+struct ForkKey {
+    int dev;
+    hipStream_t caller;
+};
+constexpr size_t kForkMax = 256;
 std::mutex g_fork_mu;
-std::vector<Fork*> g_fork;
+std::vector<std::pair<ForkKey, Fork*>> g_fork;
 
-int fork_state(Fork** out) {
+// the fork state of (current device, caller stream s); *out = nullptr when the table is full
+int fork_state(hipStream_t s, Fork** out) {
+    *out = nullptr;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     std::lock_guard<std::mutex> g(g_fork_mu);
-    if ((int)g_fork.size() <= dev) g_fork.resize((size_t)dev + 1, nullptr);
-    Fork* f = g_fork[(size_t)dev];
-    if (!f) {
-        f = new Fork();
-        e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking);
-        for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t)
-            e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming);
-        if (e != hipSuccess) {
-            delete f;
-            return hip_fail(e, "overlap stream / events");
-        }
-        g_fork[(size_t)dev] = f;
+    for (auto& kv : g_fork)
+        if (kv.first.dev == dev && kv.first.caller == s) { *out = kv.second; return 0; }
+    if (g_fork.size() >= kForkMax) return 0;
+    Fork* f = new Fork();
+    e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking);
+    for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t)
+        e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        delete f;
+        return hip_fail(e, "overlap stream / events");
     }
+    g_fork.push_back({ForkKey{dev, s}, f});
     *out = f;
     return 0;
 }
@@ -194,11 +203,14 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         q.n_pairs = n_pairs;
         q.out = out;
         q.num_cus = num_cus;
+        q.guard = gjkepa_guard_of(q);
         if ((e = gjkepa_launch_query(vert_dtype, precision, q, s)) != hipSuccess) return hip_fail(e, "query kernel launch");
         return 0;
     }
     static_assert(sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY) <= kWsHeader, "workspace header");
-    if ((e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY), s)) != hipSuccess)
+    // counter / tally reset: a one-wave kernel rather than a memset, so a captured chain is kernel
+    // nodes only
+    if ((e = gjkepa_launch_ws_reset(ctr, GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY, s)) != hipSuccess)
         return hip_fail(e, "workspace counter reset");
     uint32_t* tally = ctr + GJKEPA_WS_COUNTERS;
     int launch = 0;
@@ -216,10 +228,12 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     g.route_code = -1;                                   // GJK tier 0: every pair
     g.ctr = ctr + launch++;
     g.claim = 1;
+    g.guard = gjkepa_guard_of(g);
     if ((e = gjkepa_launch_gjk(0, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 0 launch");
     g.route_code = GJKEPA_ROUTE_GJK1;                    // GJK tier 1: hulls above tier 0's capacity
     g.ctr = ctr + launch++;
     g.claim = kSparseClaim;
+    g.guard = gjkepa_guard_of(g);
     if ((e = gjkepa_launch_gjk(1, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 1 launch");
     gjkepa_epa_args a{};
     a.version = version;
@@ -235,13 +249,17 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.num_cus = num_cus;
     // small batches (e.g. combined single-pair queries) keep one stream: the fork's events and extra
     // launches cost more latency than the overlap saves
-    const bool overlap = GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin;
+    Fork* f = nullptr;
+    int rc;
+    if (GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin && (rc = fork_state(s, &f))) return rc;
+    const bool overlap = f != nullptr;
     auto epa_tier = [&](int t) -> int {                  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
         a.ct_base = overlap ? GJKEPA_ROUTE_CT(t) : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
+        a.guard = gjkepa_guard_of(a);
         hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, s);
         return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");
     };
@@ -252,15 +270,13 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             a.next_code = -1;
             a.ctr = ctr + launch++;
             a.claim = (t == 0 && base <= GJKEPA_ROUTE_CT(0)) ? 1 : kSparseClaim;
+            a.guard = gjkepa_guard_of(a);
             hipError_t er = gjkepa_launch_contact(t, vert_dtype, precision, a, cs);
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
         }
         return 0;
     };
-    int rc;
     if (overlap) {
-        Fork* f = nullptr;
-        if ((rc = fork_state(&f))) return rc;
         std::lock_guard<std::mutex> lk(f->mu);
         for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
             if ((rc = epa_tier(t))) return rc;
@@ -466,6 +482,7 @@ Combiner* combiner(int device) {
 // copied to the device in one DMA, run, and its records copied back in one DMA.
 int run_queries_on(DeviceState* d, std::vector<Query*>& qs, int device) {
     const size_t nq = qs.size();
+    if (nq == 0) return 0;
     size_t nv = 0;
     for (Query* q : qs) nv += 3 * (size_t)(q->n1 + q->n2);
     const size_t rec = sizeof(gjkepa_contact_f64);
@@ -549,9 +566,13 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
             while ((int)cb->queue.size() < cb->inflight &&
                    cb->cv_lead.wait_until(lk, until) != std::cv_status::timeout) {
             }
+            // the queued pairs with the first one's (version_, TOL_FF_), compared bit for bit (a NaN
+            // TOL_FF_ joins its own batch); the first pair always leaves the queue
             std::vector<Query*> batch, rest;
+            const Query* q0 = cb->queue[0];
             for (Query* q : cb->queue)
-                (q->version == cb->queue[0]->version && q->tol_ff == cb->queue[0]->tol_ff ? batch : rest).push_back(q);
+                (q == q0 || (q->version == q0->version && std::memcmp(&q->tol_ff, &q0->tol_ff, sizeof(double)) == 0)
+                     ? batch : rest).push_back(q);
             cb->queue.swap(rest);
             lk.unlock();
             const auto t0 = std::chrono::steady_clock::now();

@@ -218,6 +218,7 @@ struct gjkepa_gjk_args {
     void* out;                  // contact records (hits: simplex codes parked in their slot)
     int grid;                   // <= 0: occupancy x CUs
     int num_cus;
+    uint32_t guard;             // gjkepa_guard_of(*this): checked at kernel entry in GJKEPA_DIAG_GUARD builds
 };
 
 struct gjkepa_epa_args {
@@ -238,7 +239,38 @@ struct gjkepa_epa_args {
     void* out;
     int grid;
     int num_cus;
+    uint32_t guard;             // gjkepa_guard_of(*this): checked at kernel entry in GJKEPA_DIAG_GUARD builds
 };
+
+// Kernel-argument checksum over every field but `guard` (set by the host before each launch).  A
+// GJKEPA_DIAG_GUARD build recomputes it at kernel entry: a kernel whose argument block does not
+// match what the host enqueued records the mismatch in a device-global report
+// (gjkepa_diag_guard) and returns without touching memory.
+__host__ __device__ inline uint64_t gjkepa_mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    return h;
+}
+__host__ __device__ inline uint32_t gjkepa_fold(uint64_t h) { return (uint32_t)(h ^ (h >> 32)) | 1u; }
+__host__ __device__ inline uint32_t gjkepa_guard_of(const gjkepa_gjk_args& a) {
+    uint64_t h = 0x67ull;
+    h = gjkepa_mix(h, (uint64_t)a.verts); h = gjkepa_mix(h, (uint64_t)a.hull_off); h = gjkepa_mix(h, (uint64_t)a.hull_cnt);
+    h = gjkepa_mix(h, (uint64_t)a.pairs); h = gjkepa_mix(h, (uint64_t)a.n_pairs); h = gjkepa_mix(h, (uint64_t)a.route);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.route_code); h = gjkepa_mix(h, (uint64_t)a.ctr);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.claim); h = gjkepa_mix(h, (uint64_t)a.tally); h = gjkepa_mix(h, (uint64_t)a.warm);
+    h = gjkepa_mix(h, (uint64_t)a.out); h = gjkepa_mix(h, (uint64_t)(int64_t)a.grid); h = gjkepa_mix(h, (uint64_t)(int64_t)a.num_cus);
+    return gjkepa_fold(h);
+}
+__host__ __device__ inline uint32_t gjkepa_guard_of(const gjkepa_epa_args& a) {
+    uint64_t h = 0x65ull;
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.version); h = gjkepa_mix(h, __builtin_bit_cast(uint64_t, a.tol_ff));
+    h = gjkepa_mix(h, (uint64_t)a.verts); h = gjkepa_mix(h, (uint64_t)a.hull_off); h = gjkepa_mix(h, (uint64_t)a.hull_cnt);
+    h = gjkepa_mix(h, (uint64_t)a.pairs); h = gjkepa_mix(h, (uint64_t)a.n_pairs); h = gjkepa_mix(h, (uint64_t)a.route);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.route_code); h = gjkepa_mix(h, (uint64_t)(int64_t)a.next_code);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.ct_base); h = gjkepa_mix(h, (uint64_t)a.ctr);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.claim); h = gjkepa_mix(h, (uint64_t)a.tally); h = gjkepa_mix(h, (uint64_t)a.out);
+    h = gjkepa_mix(h, (uint64_t)(int64_t)a.grid); h = gjkepa_mix(h, (uint64_t)(int64_t)a.num_cus);
+    return gjkepa_fold(h);
+}
 
 hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s);
 hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
@@ -246,3 +278,5 @@ hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjke
 hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
 // one-kernel path for small batches: one wave per pair (grid = n_pairs), GJK + EPA + contact features
 hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
+// the chain's counter / tally reset (n32 uint32 words from ws); a kernel node rather than a memset node
+hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s);

@@ -73,6 +73,29 @@ DEV void stamp_end() {
 #define GK_STAMP_BEGIN() ((void)0)
 #define GK_STAMP_END() ((void)0)
 #endif
+// ---------------------------------------------------------------- diagnostic argument guard
+// Built only with -DGJKEPA_DIAG_GUARD: every kernel recomputes its argument block's checksum
+// (gjkepa_guard_of) at entry; on a mismatch it counts the event in g_guard (read by
+// gjkepa_diag_guard) and returns before any memory access the arguments describe.
+#ifdef GJKEPA_DIAG_GUARD
+__device__ uint32_t g_guard[8];   // [0] mismatches, [1] kernel id << 8 | route code, [2] expected, [3] recomputed
+DEV void guard_report(uint32_t kid, uint32_t want, uint32_t got) {
+    if (lane_id() == 0) {
+        atomicAdd(&g_guard[0], 1u);
+        atomicExch(&g_guard[1], kid);
+        atomicExch(&g_guard[2], want);
+        atomicExch(&g_guard[3], got);
+    }
+}
+#define GK_GUARD(kid, code)                                                                   \
+    do {                                                                                     \
+        const uint32_t g_ = gjkepa_guard_of(a);                                              \
+        if (g_ != a.guard) { guard_report(((uint32_t)(kid) << 8) | ((uint32_t)(code) & 0xffu), a.guard, g_); return; } \
+    } while (0)
+#else
+#define GK_GUARD(kid, code) ((void)0)
+#endif
+
 enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
        SE_LOAD = 10, SE_IT1, SE_DIR, SE_SUP, SE_VIS, SE_HOR, SE_CMP, SE_CONE, SE_TERM, SE_NEAR, SE_CONT, SE_TYPE,
        SE_STORE, SE_ROUTE };
@@ -1586,6 +1609,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
+    GK_GUARD(1, a.route_code);
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
@@ -1664,6 +1688,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
+    GK_GUARD(2, a.route_code);
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
@@ -1770,6 +1795,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     const int gl = grp.gl;
     const int gid = grp.lane / G;
     const TIn* verts = (const TIn*)a.verts;
+    GK_GUARD(3, a.route_code);
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
@@ -1865,6 +1891,7 @@ __global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
     const Grp<G> grp;
     const int gl = grp.gl;
     const int64_t pair = blockIdx.x;
+    GK_GUARD(5, 0);
     if (pair >= a.n_pairs) return;
     const TIn* verts = (const TIn*)a.verts;
     Ctx<T, TIn, G, K, VC, FC, 2> c{L, grp};
@@ -1926,6 +1953,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     L_t& L = *reinterpret_cast<L_t*>(smem + lds_stride<L_t, G>() * (grp.lane / G));
     const int gl = grp.gl;
     const TIn* verts = (const TIn*)a.verts;
+    GK_GUARD(4, a.route_code);
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
@@ -1965,6 +1993,16 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     GK_STAMP(SE_ROUTE);
     tally_end(a.tally);
     GK_STAMP_END();
+}
+
+// Counter / tally reset at the head of a chain (one wave; the chain's first node).
+__global__ __launch_bounds__(64) void ws_reset_kernel(uint32_t* ws, int n32, uint32_t guard) {
+#ifdef GJKEPA_DIAG_GUARD
+    const uint32_t g_ = gjkepa_fold(gjkepa_mix(gjkepa_mix(0x72ull, (uint64_t)ws), (uint64_t)(int64_t)n32));
+    if (g_ != guard) { guard_report(6u << 8, guard, g_); return; }
+#endif
+    (void)guard;
+    for (int i = (int)threadIdx.x; i < n32; i += 64) ws[i] = 0u;
 }
 
 }  // namespace gk
@@ -2047,6 +2085,25 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s) {
+    const uint32_t guard = gjkepa_fold(gjkepa_mix(gjkepa_mix(0x72ull, (uint64_t)ws), (uint64_t)(int64_t)n32));
+    hipLaunchKernelGGL(gk::ws_reset_kernel, dim3(1), dim3(64), 0, s, ws, n32, guard);
+    return hipGetLastError();
+}
+
+#ifdef GJKEPA_DIAG_GUARD
+// diagnostic build only: the argument-guard report ([0] mismatches, [1] kernel id << 8 | route
+// code of the last, [2] expected and [3] recomputed checksum), optionally cleared
+extern "C" int gjkepa_diag_guard(uint32_t* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gk::g_guard), sizeof(gk::g_guard)) != hipSuccess) return -1;
+    if (reset) {
+        uint32_t z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gk::g_guard), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 8;
+}
+#endif
 
 #ifdef GJKEPA_DIAG_STAMPS
 // diagnostic build only: read (and optionally clear) the phase stamp totals

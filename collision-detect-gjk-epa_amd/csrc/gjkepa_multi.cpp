@@ -103,11 +103,17 @@ int gjkepa_batch_multi(int32_t version, double tol_ff, int32_t vert_dtype, int32
         return set_error(GJKEPA_E_ARG, "bad dtype/precision");
     if (n_pairs == 0) return 0;
     if (!verts || !hull_off || !hull_cnt || !pairs || !out) return set_error(GJKEPA_E_ARG, "null pointer");
-    for (int i = 0; i < ndev; ++i)
-        for (int j = 0; j < i; ++j)
-            if (devices[i] == devices[j]) return set_error(GJKEPA_E_ARG, "device listed twice");
+    // the same argument checks as one gjkepa_batch call over the whole job, before any shard runs
+    // (a shard's own call sees only its rebased slice of the pool)
     for (int64_t k = 0; k < 2 * n_pairs; ++k)
         if (pairs[k] < 0 || pairs[k] >= n_hulls) return set_error(GJKEPA_E_ARG, "pair references a missing hull");
+    for (int64_t h = 0; h < n_hulls; ++h) {
+        const int64_t c = hull_cnt[h];
+        if (c >= 1 && (hull_off[h] < 0 || hull_off[h] + 3 * c > n_vert_scalars))
+            return set_error(GJKEPA_E_ARG, "hull outside the vertex pool");
+    }
+    // A device may be listed more than once: its shards then run one after the other (gjkepa_batch
+    // serialises the calls on one device), which also lets one GPU run any shard count.
     const size_t esz = vert_dtype == GJKEPA_DTYPE_F32 ? 4 : 8;
     std::vector<int> rc((size_t)ndev, 0);
     std::vector<std::string> msg((size_t)ndev);

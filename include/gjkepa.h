@@ -278,7 +278,9 @@ int gjkepa_shard_range(int64_t n_pairs, int32_t world, int32_t rank, int64_t* fi
 /* One process, several devices (host buffers, blocking): gjkepa_batch's arguments plus a device list.
  * Shard s (gjkepa_shard_range over ndev) runs on devices[s] from its own host thread; only the hulls
  * the shard references are copied to that device; its records land at out[first .. first + count),
- * so `out` holds every record in pair order — bit-identical to one gjkepa_batch call. */
+ * so `out` holds every record in pair order — bit-identical to one gjkepa_batch call.  The argument
+ * checks are gjkepa_batch's, over the whole job, before any shard runs.  A device may appear more
+ * than once: its shards then run one after the other. */
 int gjkepa_batch_multi(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
                        const void* verts, int64_t n_vert_scalars,
                        const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,

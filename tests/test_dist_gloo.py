@@ -108,10 +108,19 @@ def test_library_shard_range_tiles_the_job(world):
 
 
 def test_multi_device_argument_checks():
-    """gjkepa_batch_multi rejects a bad device list before touching any device."""
+    """gjkepa_batch_multi rejects an empty device list and a pool that one gjkepa_batch call would
+    reject (a pair naming a missing hull, a hull outside the vertex pool) before touching any device."""
     import gjkepa
 
     pool = gjkepa.synth_pairs(0x6A4B5C1D, 4, 8, 8, 2.5)
-    for devs in ([], [0, 0]):
-        with pytest.raises(gjkepa.GjkEpaError):
-            gjkepa.gjkepa_batch_multi(pool, devs)
+    with pytest.raises(gjkepa.GjkEpaError, match="device list"):
+        gjkepa.gjkepa_batch_multi(pool, [])
+    bad_pair = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs.copy())
+    bad_pair.pairs[3, 1] = len(pool.hull_cnt)
+    with pytest.raises(gjkepa.GjkEpaError, match="missing hull"):
+        gjkepa.gjkepa_batch_multi(bad_pair, [0, 0])
+    for off in (-3, len(pool.verts) - 3 * int(pool.hull_cnt[5]) + 1):   # 1-based slip / past the end
+        o = pool.hull_off.copy()
+        o[5] = off
+        with pytest.raises(gjkepa.GjkEpaError, match="outside the vertex pool"):
+            gjkepa.gjkepa_batch_multi(gjkepa.HullPool(pool.verts, o, pool.hull_cnt, pool.pairs), [0, 0, 0])

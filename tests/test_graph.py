@@ -1,12 +1,7 @@
 """gjkepa_batch_device is graph-capturable (include/gjkepa.h): the whole launch chain — counter reset,
-the tier kernels and the contact pass forked onto the library's second stream and joined back —
-captured into a HIP graph and replayed gives the records of a direct call, byte for byte, replay
-after replay.
-
-Opt-in (GJKEPA_GRAPH_TEST=1): run alone it passes, but in two of three full `-m gpu` sessions the
-first replay faulted (illegal address) after the other GPU tests had run in the same process, with
-the same build passing standalone and in the third session.  The cause is not found,
-so the default suite does not risk a GPU fault on it."""
+the tier kernels and (for batches of 64K pairs and up) the contact passes forked onto the library's
+second stream and joined back — captured into a HIP graph and replayed gives the records of a
+direct call, byte for byte, replay after replay."""
 import os
 
 import numpy as np
@@ -14,16 +9,29 @@ import pytest
 
 import gjkepa
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("GJKEPA_GRAPH_TEST") != "1", reason="opt-in: GJKEPA_GRAPH_TEST=1")]
+pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("lo,hi,rmax", [(32, 32, 2.5), (8, 256, 2.5)])
-def test_captured_chain_replays_bitexact(lo, hi, rmax):
+REPLAYS = int(os.environ.get("GJKEPA_GRAPH_REPLAYS", "10"))
+
+
+def _guard_report():
+    """Argument-guard report of a GJKEPA_DIAG_GUARD build (tools/build_variant.sh guard), else None."""
+    import ctypes
+    lib = gjkepa.load()
+    if not hasattr(lib, "gjkepa_diag_guard"):
+        return None
+    out = (ctypes.c_uint32 * 8)()
+    assert lib.gjkepa_diag_guard(out, 1) == 8
+    return list(out)
+
+
+@pytest.mark.parametrize("lo,hi,rmax,n", [(32, 32, 2.5, 3000), (8, 256, 2.5, 3000), (32, 32, 2.5, 70000)])
+@pytest.mark.parametrize("prec", [gjkepa.PREC_F32, gjkepa.PREC_F64], ids=["f32", "f64"])
+def test_captured_chain_replays_bitexact(lo, hi, rmax, n, prec):
     import torch
     dev = torch.device("cuda", 0)
-    pool = gjkepa.synth_pairs(0x5EED, 3000, lo, hi, rmax, dtype=np.float32)
-    n = pool.n_pairs
+    pool = gjkepa.synth_pairs(0x5EED, n, lo, hi, rmax, dtype=np.float32)
     verts = torch.from_numpy(pool.verts).to(dev)
     off = torch.from_numpy(pool.hull_off).to(dev)
     cnt = torch.from_numpy(pool.hull_cnt).to(dev)
@@ -32,12 +40,14 @@ def test_captured_chain_replays_bitexact(lo, hi, rmax):
     ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
 
     def run(out, stream):
-        gjkepa.gjkepa_batch_device(2, 1.0, gjkepa.DTYPE_F32, gjkepa.PREC_F64, verts.data_ptr(), off.data_ptr(),
+        gjkepa.gjkepa_batch_device(2, 1.0, gjkepa.DTYPE_F32, prec, verts.data_ptr(), off.data_ptr(),
                                    cnt.data_ptr(), prs.data_ptr(), n, out.data_ptr(), ws.data_ptr(), wsb, stream)
 
     work = torch.cuda.Stream(dev)
-    ref = torch.zeros(n * 128, dtype=torch.uint8, device=dev)
+    ref = torch.zeros(n * (128 if prec == gjkepa.PREC_F64 else 64), dtype=torch.uint8, device=dev)
     out = torch.zeros_like(ref)
+    for name, t in (("verts", verts), ("off", off), ("cnt", cnt), ("pairs", prs), ("ws", ws), ("ref", ref), ("out", out)):
+        print(f"graph-test buffer {name}: {t.data_ptr():#x} + {t.numel() * t.element_size()} B", flush=True)
     torch.cuda.synchronize(dev)
     with torch.cuda.stream(work):
         run(ref, work.cuda_stream)
@@ -47,11 +57,23 @@ def test_captured_chain_replays_bitexact(lo, hi, rmax):
     with torch.cuda.graph(g, stream=side):
         run(out, side.cuda_stream)
     torch.cuda.synchronize(dev)
-    for _ in range(3):
+    for i in range(REPLAYS):
+        print(f"graph-test replay {i}", flush=True)
         with torch.cuda.stream(work):
             out.zero_()
             g.replay()
         torch.cuda.synchronize(dev)
+        rep = _guard_report()
+        if rep is not None:
+            print(f"graph-test guard after replay {i}: {rep}", flush=True)
+            assert rep[0] == 0, f"kernel argument block changed after enqueue: {rep}"
         assert torch.equal(out, ref)
-    expect = gjkepa.gjkepa_batch(pool, 2, 1.0)
-    assert np.frombuffer(ref.cpu().numpy().tobytes(), dtype=gjkepa.REC64).tobytes() == expect.tobytes()
+    # a direct call after the replays still matches (the graph left no state behind)
+    with torch.cuda.stream(work):
+        out.zero_()
+        run(out, work.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(out, ref)
+    expect = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=prec)
+    assert ref.cpu().numpy().tobytes() == expect.tobytes()
+    del g

@@ -3,8 +3,9 @@
 - C3 per-rank workload: each of two ranks owns 2^21 C2-distribution pairs at first_pair = r * 2^21
   (the library's shard rule); each shard, run through the C-ABI on the GPU, is byte-identical to the
   matching half of one contiguous 2^22-pair run and to the oracle on a subsample.
-- gjkepa_batch_multi (one process, a device list) equals gjkepa_batch; the box has one GPU, so the
-  list holds device 0 (the shard / rebase / thread path is the same for any length).
+- gjkepa_batch_multi (one process, a device list) equals gjkepa_batch and the oracle.  The box has
+  one GPU, so the lists repeat device 0 (2, 3 and 8 shards): every shard still goes through the
+  shard / hull-range rebase / per-shard thread path, and the shards of one device run in turn.
 - The library's RCCL communicator (world 1 here; the driver's 8-GPU run exercises world 8): the
   in-place and out-of-place all-gather of records returns them unchanged.
 """
@@ -37,23 +38,40 @@ def test_c3_rank_shards_match_contiguous_run_and_oracle(orc):
         assert got[sub].tobytes() == o.tobytes(), rank
 
 
+@pytest.mark.parametrize("ndev", [1, 2, 3, 8])
 @pytest.mark.parametrize("lo,hi", [(32, 32), (8, 256)])
-def test_batch_multi_matches_batch(lo, hi):
-    pool = gjkepa.synth_pairs(SEED, 50000, lo, hi, 2.5)
+def test_batch_multi_matches_batch(lo, hi, ndev, orc):
+    """Contiguous pairs (each pair owns its hulls) in ndev shards on device 0."""
+    pool = gjkepa.synth_pairs(SEED, 50001, lo, hi, 2.5)       # odd size: shards differ by one pair
     a = gjkepa.gjkepa_batch(pool, 2, 1.0)
-    b = gjkepa.gjkepa_batch_multi(pool, [0], 2, 1.0)
+    b = gjkepa.gjkepa_batch_multi(pool, [0] * ndev, 2, 1.0)
     assert a.tobytes() == b.tobytes()
+    sub = np.arange(0, pool.n_pairs, 211)
+    o = orc.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[sub]), 2, 1.0)
+    assert b[sub].tobytes() == o.tobytes()
 
 
-def test_batch_multi_shared_hull_pool(orc):
-    """A pool whose pairs share hulls out of order (a broad-phase list): each shard copies only the
-    hull range it references, rebased; results equal the oracle."""
+@pytest.mark.parametrize("ndev", [1, 2, 3, 8])
+def test_batch_multi_shared_hull_pool(orc, ndev):
+    """A pool whose pairs share hulls out of order (a broad-phase list): every shard's hull range
+    straddles the others'; each shard copies only the range it references, rebased.  Equal to one
+    gjkepa_batch call and to the oracle."""
     rng = np.random.default_rng(3)
     hulls = gjkepa.synth_pairs(SEED, 300, 8, 64, 2.5)
     prs = rng.integers(0, 600, size=(4000, 2)).astype(np.int32)
     pool = gjkepa.HullPool(hulls.verts, hulls.hull_off, hulls.hull_cnt, prs)
-    g = gjkepa.gjkepa_batch_multi(pool, [0], 2, 1.0)
+    g = gjkepa.gjkepa_batch_multi(pool, [0] * ndev, 2, 1.0)
+    assert g.tobytes() == gjkepa.gjkepa_batch(pool, 2, 1.0).tobytes()
     assert g.tobytes() == orc.gjkepa_batch(pool, 2, 1.0).tobytes()
+
+
+def test_batch_multi_rejects_hull_outside_pool():
+    """The whole-job argument checks of gjkepa_batch apply before sharding."""
+    pool = gjkepa.synth_pairs(SEED, 64, 8, 32, 2.5)
+    off = pool.hull_off.copy()
+    off[7] = len(pool.verts)
+    with pytest.raises(gjkepa.GjkEpaError, match="outside the vertex pool"):
+        gjkepa.gjkepa_batch_multi(gjkepa.HullPool(pool.verts, off, pool.hull_cnt, pool.pairs), [0, 0])
 
 
 def test_rccl_comm_world1_allgather():

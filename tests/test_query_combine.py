@@ -59,3 +59,15 @@ def test_concurrent_query_error_reaches_its_caller():
     for i, c in enumerate(got):
         if i % 8 == 0:
             assert c.status == gjkepa.STATUS_BAD_INPUT and not c.collision
+
+
+@pytest.mark.gpu
+def test_concurrent_queries_nan_tolerance(orc):
+    """A NaN TOL_FF_ never equals itself: the combiner still moves the first queued pair into its
+    batch (compared bit for bit) instead of leaving it queued forever.  Mixed versions,
+    finite and NaN tolerances from 12 threads; every caller gets the oracle's record."""
+    qs = [(v, t, a, b) for (v, _, a, b), t in zip(_pairs(240, 11), [1.0, float("nan"), 1e-3, float("nan")] * 60)]
+    with cf.ThreadPoolExecutor(12) as ex:
+        got = list(ex.map(lambda q: gjkepa.gjkepa(q[0], q[1], q[2], q[3]), qs))
+    bad = [i for i, (q, c) in enumerate(zip(qs, got)) if not _same(c, orc.gjkepa(q[0], q[1], q[2], q[3]))]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
