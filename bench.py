@@ -3,9 +3,10 @@
 
 Workload (N=1) = BASELINE config C2: 2^20 random 32-vertex convex-hull pairs, fp32 vertex storage,
 version_=2, TOL_FF_=1.0, hull B centre offset r ~ U[0, 2.5] (seed 0x6A4B5C1D).
+N>1 defaults to config C3: the same distribution, 2^21 pairs per GPU (2^24 on 8 GPUs).
 A "step" is one pass of the hot path (gjkepa_batch_device: the tiered GJK/EPA kernels) over the
 whole batch, with hulls, pair list and output already resident in HBM.  For N > 1 each rank owns
-a contiguous shard of `--pairs-per-gpu` pairs (weak scaling; the library's gjkepa_shard_range) and
+a contiguous shard of the config's pairs per GPU (weak scaling; the library's gjkepa_shard_range) and
 every step's contact records are all-gathered over xGMI by the library's RCCL communicator
 (gjkepa_comm_* / gjkepa_allgather_records_device: config C3's exchange).  The gather of step i runs
 on its own stream while step i+1's kernels run (two record buffers, gathered in place); the timed
@@ -41,6 +42,8 @@ METRIC = "M convex-pair GJK+EPA queries/sec at 1/2/4/8 MI355X; % HBM roofline"
 # BASELINE.json configs: (hull n_min, n_max, centre offset r_max, default pairs per GPU)
 CONFIGS = {
     "C2": (32, 32, 2.5, 1 << 20, "1M random 32-vertex convex-hull pairs"),
+    "C3": (32, 32, 2.5, 1 << 21, "C2 distribution, 2^21 32-vertex pairs per GPU (16M on 8 GPUs), "
+                                 "contact records all-gathered over xGMI"),
     "C4": (8, 256, 2.5, 4 << 20, "4M pairs, mixed hull sizes 8-256 vertices"),
     "C5": (32, 128, 0.3, 1 << 20, "deep-overlap pairs (r~U[0,0.3]), 32-128-vertex hulls, EPA-heavy"),
 }
@@ -99,7 +102,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="default: C2 on one GPU, C3 (2^21 pairs per GPU + all-gather) when --gpus > 1")
     ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: the config's size")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 record exchange: nccl = the library's RCCL all-gather, gloo = host-staged rehearsal")
@@ -133,6 +137,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     lib = gjkepa.load()
 
+    if args.config is None:
+        args.config = "C3" if max(world, args.gpus) > 1 else "C2"
     nmin, nmax, rmax, n_default, desc = CONFIGS[args.config]
     n = args.pairs_per_gpu or n_default
     prec = gjkepa.PREC_F64 if args.precision == "f64" else gjkepa.PREC_F32

@@ -130,10 +130,27 @@ int num_cus_current() {
 // Up to kForkMax caller streams get their own; further streams run the chain on one stream.
 // (A/B: the other way round, later EPA tiers on a high-priority internal stream beside the contact
 // pass, was 2.5% slower on C2.)
+// Each fork point gets its own internal stream (GJKEPA_FORK_STREAMS 2; 1: one shared stream, the
+// passes in order), so a small pass forked late does not queue behind the big pass of tier 0.  The
+// internal streams run at the lowest stream priority (GJKEPA_FORK_LOWPRIO): the EPA tiers on the
+// caller's stream are dispatched first as the pass's workgroups free wave slots.  The last fork
+// point's pass runs on the caller's stream (GJKEPA_LAST_PASS_MAIN): nothing follows it to overlap.
+#ifndef GJKEPA_FORK_MASK
+#define GJKEPA_FORK_MASK 0x15
+#endif
+#ifndef GJKEPA_FORK_STREAMS
+#define GJKEPA_FORK_STREAMS 2
+#endif
+#ifndef GJKEPA_FORK_LOWPRIO
+#define GJKEPA_FORK_LOWPRIO 1
+#endif
+#ifndef GJKEPA_LAST_PASS_MAIN
+#define GJKEPA_LAST_PASS_MAIN 1
+#endif
 struct Fork {
     std::mutex mu;
-    hipStream_t s2 = nullptr;
-    hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join = nullptr;
+    hipStream_t s2[GJKEPA_EPA_TIERS] = {};       // internal stream of fork point t (all [0] if shared)
+    hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join[GJKEPA_EPA_TIERS] = {};
 };
 struct ForkKey {
     int dev;
@@ -154,10 +171,16 @@ int fork_state(hipStream_t s, Fork** out) {
         if (kv.first.dev == dev && kv.first.caller == s) { *out = kv.second; return 0; }
     if (g_fork.size() >= kForkMax) return 0;
     Fork* f = new Fork();
-    e = hipStreamCreateWithFlags(&f->s2, hipStreamNonBlocking);
-    for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t)
-        e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming);
+    int least = 0, greatest = 0;
+    if (!GJKEPA_FORK_LOWPRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t) {
+        // a stream per fork point that forks (the first one only when shared)
+        const bool forks = ((GJKEPA_FORK_MASK >> t) & 1) && !(GJKEPA_LAST_PASS_MAIN && t == GJKEPA_EPA_TIERS - 1);
+        if (forks && (GJKEPA_FORK_STREAMS > 1 || !f->s2[0])) e = hipStreamCreateWithPriority(&f->s2[t], hipStreamNonBlocking, least);
+        else if (forks) f->s2[t] = f->s2[0];
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[t], hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         delete f;
         return hip_fail(e, "overlap stream / events");
@@ -173,14 +196,40 @@ constexpr int epa_hull_cap(int t) {
          : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : GJKEPA_E4_G * GJKEPA_E4_K;
 }
 
-// launches of an overlapped chain: 2 GJK + the EPA tiers + each EPA tier's contact pass; every
+// Fork points of an overlapped chain (bit t: a contact pass is forked after EPA tier t).  The pairs
+// EPA tier t finishes go to the contact pass of the first fork point p >= t (route code
+// GJKEPA_ROUTE_CT(p) + contact tier).  Default: after tier 0 (C2's hits), after tier 2 (C4 / C5's
+// 33-128-vertex hulls, with tier 1's few overflow pairs) and after the last tier (tiers 3-4): three
+// forks and five contact launches instead of one fork and up to two launches per tier, so the short
+// tail of a C2 chain carries three fewer near-empty launches.
+static_assert((GJKEPA_FORK_MASK >> (GJKEPA_EPA_TIERS - 1)) & 1, "the last EPA tier is a fork point");
+constexpr int fork_point(int t) {          // first fork point >= t
+    while (!((GJKEPA_FORK_MASK >> t) & 1)) ++t;
+    return t;
+}
+// contact tiers a fork point's pass needs: 1 when every hull of its EPA tiers fits contact tier 0
+constexpr int fork_contact_tiers(int p) {
+    int cap = 0;
+    for (int t = 0; t <= p; ++t)
+        if (fork_point(t) == p && epa_hull_cap(t) > cap) cap = epa_hull_cap(t);
+    return cap <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
+}
+// launches of an overlapped chain: 2 GJK + the EPA tiers + each fork point's contact pass; every
 // launch owns one workspace counter
 constexpr int overlap_launches() {
     int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS;
-    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) n += epa_hull_cap(t) <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
+    for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
+        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t);
     return n;
 }
 static_assert(overlap_launches() <= GJKEPA_WS_COUNTERS, "workspace launch counters");
+// The forked contact pass of EPA tier 0 (a dense launch) takes one workgroup per 64-pair chunk
+// instead of an occupancy-sized grid of looping workgroups: a workgroup leaves when its chunk is
+// done, so the EPA tiers launched beside the pass get wave slots as they free up instead of
+// queueing behind the whole pass (C2: the empty EPA tier 2 launch waited 657 us behind it).
+#ifndef GJKEPA_CONTACT_UNITS_GRID
+#define GJKEPA_CONTACT_UNITS_GRID 1
+#endif
 
 int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
@@ -256,9 +305,10 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     auto epa_tier = [&](int t) -> int {                  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
-        a.ct_base = overlap ? GJKEPA_ROUTE_CT(t) : GJKEPA_ROUTE_CT0;
+        a.ct_base = overlap ? GJKEPA_ROUTE_CT(fork_point(t)) : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
+        a.grid = 0;
         a.guard = gjkepa_guard_of(a);
         hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, s);
         return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");
@@ -270,6 +320,8 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             a.next_code = -1;
             a.ctr = ctr + launch++;
             a.claim = (t == 0 && base <= GJKEPA_ROUTE_CT(0)) ? 1 : kSparseClaim;
+            // a forked dense pass (EPA tier 0's hits) takes one workgroup per chunk
+            a.grid = GJKEPA_CONTACT_UNITS_GRID && cs != s && a.claim == 1 ? GJKEPA_GRID_UNITS : 0;
             a.guard = gjkepa_guard_of(a);
             hipError_t er = gjkepa_launch_contact(t, vert_dtype, precision, a, cs);
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
@@ -278,16 +330,28 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     };
     if (overlap) {
         std::lock_guard<std::mutex> lk(f->mu);
+        constexpr int last = GJKEPA_EPA_TIERS - 1;
+        bool forked[GJKEPA_EPA_TIERS] = {};
         for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
             if ((rc = epa_tier(t))) return rc;
-            if ((e = hipEventRecord(f->fork[t], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2, f->fork[t], 0)) != hipSuccess)
+            if (!((GJKEPA_FORK_MASK >> t) & 1)) continue;
+            if (GJKEPA_LAST_PASS_MAIN && t == last) {
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), s))) return rc;
+                continue;
+            }
+            if ((e = hipEventRecord(f->fork[t], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[t], f->fork[t], 0)) != hipSuccess)
                 return hip_fail(e, "contact pass fork");
-            // an EPA tier whose hulls all fit contact tier 0 produces no contact-tier-1 pairs
-            const int nct = epa_hull_cap(t) <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
-            if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), nct, f->s2))) return rc;
+            if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), f->s2[t]))) return rc;
+            forked[t] = true;
         }
-        if ((e = hipEventRecord(f->join, f->s2)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join, 0)) != hipSuccess)
-            return hip_fail(e, "contact pass join");
+        for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {      // join every internal stream used (last one per stream)
+            if (!forked[t]) continue;
+            bool later = false;
+            for (int u = t + 1; u < GJKEPA_EPA_TIERS; ++u) later = later || (forked[u] && f->s2[u] == f->s2[t]);
+            if (later) continue;
+            if ((e = hipEventRecord(f->join[t], f->s2[t])) != hipSuccess || (e = hipStreamWaitEvent(s, f->join[t], 0)) != hipSuccess)
+                return hip_fail(e, "contact pass join");
+        }
         return 0;
     }
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)

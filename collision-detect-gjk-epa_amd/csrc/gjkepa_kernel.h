@@ -203,6 +203,10 @@
 // with GJKEPA_CONTACT_OVERLAP, the pairs EPA tier t finishes go to contact tier c under code CT(t) + c
 #define GJKEPA_ROUTE_CT(t) (GJKEPA_ROUTE_CT0 + 2 * (t))
 
+// gjkepa_*_args::grid: > 0 explicit, 0 occupancy x CUs (looping workgroups), GJKEPA_GRID_UNITS one
+// workgroup per work unit
+#define GJKEPA_GRID_UNITS (-2)
+
 struct gjkepa_gjk_args {
     const void* verts;
     const int64_t* hull_off;

@@ -1494,8 +1494,8 @@ DEV uint32_t match16(uint4 v, uint32_t code) {
 struct Units {
     int64_t n_pairs, nbig, nunits;
     int small;
-    DEV Units(int64_t n, int small_) : n_pairs(n), small(small_) {
-        int64_t tail = (int64_t)gridDim.x * 64;
+    DEV Units(int64_t n, int small_, bool whole_chunks = false) : n_pairs(n), small(small_) {
+        int64_t tail = whole_chunks ? 0 : (int64_t)gridDim.x * 64;
         if (tail > n / 2) tail = n / 2;
         nbig = (n - tail) / 64;
         nunits = nbig + (n - nbig * 64 + small - 1) / small;
@@ -1541,11 +1541,24 @@ DEV int pick_claim(const uint32_t* tally, int route_code, int64_t n_pairs, int c
 
 template <int G, typename F>
 DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code,
-                              uint32_t* ctr, int claim, F&& f) {
+                              uint32_t* ctr, int claim, bool unit_grid, F&& f) {
     // the first unit of workgroup b is unit b; later units come from the counter (offset by the
-    // grid), so a launch with fewer units than workgroups issues no atomics at all
+    // grid), so a launch with fewer units than workgroups issues no atomics at all.  unit_grid: the
+    // launch has one workgroup per 64-pair chunk (dense launches only): a workgroup takes its own
+    // chunk and leaves.
     const int64_t nchunks = (n_pairs + 63) / 64;
     uint32_t next = 0;
+    if (unit_grid) {
+        const int64_t u = blockIdx.x;
+        if (u < nchunks) {
+            const int64_t p0 = u * 64;
+            const int len = n_pairs - p0 < 64 ? (int)(n_pairs - p0) : 64;
+            const uint64_t m = route_code < 0 ? (len >= 64 ? ~0ull : ((1ull << len) - 1ull))
+                                              : __ballot(grp.lane < len && (int)route[p0 + grp.lane] == route_code);
+            groups_take(grp, p0, m, f);
+        }
+        return;
+    }
     if (claim <= 1 || route_code < 0) {
         const Units U(n_pairs, tail_unit<G, (64 / G > 8 ? 64 / G : 8)>(n_pairs));
         if ((int64_t)blockIdx.x < U.nunits && grp.lane == 0) next = gridDim.x + atomicAdd(ctr, 1u);
@@ -1614,7 +1627,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, [&](int64_t pair) {
         GK_STAMP(SG_ROUTE);
         Ctx<T, TIn, G, K, 0, 0, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1693,7 +1706,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -1958,7 +1971,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, [&](int64_t pair) {
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, a.grid == GJKEPA_GRID_UNITS, [&](int64_t pair) {
         GK_STAMP(SE_ROUTE);
         Ctx<T, TIn, G, K, 0, 1, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
@@ -2062,8 +2075,12 @@ hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH>;
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 1>, G>() * GPW;
-    int grid = grid_for(kfn, lds, a.num_cus, a.grid);
-    grid = grid_cap<G>(a.n_pairs, grid);
+    int grid;
+    if (a.grid == GJKEPA_GRID_UNITS) {                  // one workgroup per 64-pair chunk (dense launches)
+        grid = (int)((a.n_pairs + 63) / 64);
+    } else {
+        grid = grid_cap<G>(a.n_pairs, grid_for(kfn, lds, a.num_cus, a.grid));
+    }
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
