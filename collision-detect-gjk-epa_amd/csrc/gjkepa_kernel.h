@@ -144,6 +144,12 @@
 #ifndef GJKEPA_LDS_SKEW
 #define GJKEPA_LDS_SKEW 1           // pad LDS coordinate columns and skew group images across banks (0: A/B off)
 #endif
+#ifndef GJKEPA_HULL_AOS
+#define GJKEPA_HULL_AOS 0           // 1: LDS hull copy as one (x, y, z, 0) 16-byte record per vertex (A/B: EPA tier 0 +13%, GJK +7%: bank conflicts)
+#endif
+#ifndef GJKEPA_SCREEN_MIN_K
+#define GJKEPA_SCREEN_MIN_K 8       // fp32-screened support mapping in tiers with K >= this (fp64 compute,
+#endif                              // fp32 storage); 0 = off
 #ifndef GJKEPA_AXIS_REJECT
 #define GJKEPA_AXIS_REJECT 0        // diagnostic A/B only, never the product build: GJK answers "miss"
                                     // when the centre axis separates the hulls.  Not parity-safe: the

@@ -106,6 +106,10 @@ enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
 // VC == 0 is the GJK kernel (FC == 0) or the contact kernel (FC == 1), which carry only their own
 // scratch, so a 16-pair GJK wave does not pay for polytope or contact arrays.
 // FUSED: the one-kernel query path (query_kernel) keeps the contact arrays beside the polytope.
+// One hull vertex in LDS (GJKEPA_HULL_AOS): x, y, z and a zero pad, so a lane fetches a whole
+// vertex with one ds_read_b128 (fp32 storage) instead of three ds_read_b32 from three columns.
+template <typename TH> struct alignas(16) HV { TH x, y, z, w; };
+
 template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = false> struct Lds {
     static constexpr int NH = G * K;
     // Coordinate columns are NH + 1 elements apart, so the six columns (hull A/B x, y, z) start on
@@ -113,7 +117,11 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
     static constexpr int NHP = NH + GJKEPA_LDS_SKEW;
     static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 && !GJKEPA_EPA_PLACE ? G : 1;
     static constexpr int NC = ((VC_ == 0 && FC_ == 1) || FUSED) ? NH : 1;
+#if GJKEPA_HULL_AOS
+    HV<TH> hv[2][NH];                       // hull A (0) / B (1) vertex i, storage precision
+#else
     TH hx[2][NHP], hy[2][NHP], hz[2][NHP];  // hull A (0) / B (1) vertices, storage precision
+#endif
     union U {
         struct E {                       // EPA polytope (faces themselves are in registers)
             T vx[VC], vy[VC], vz[VC];    // vertices by id
@@ -143,11 +151,21 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
 // the 32 four-byte banks, so group g's lane l and group g+1's lane l, touching the same field, hit
 // different banks; an unpadded image size is often a multiple of 16 or 32 dwords, which puts every
 // group of a half on the same banks (GJK tier 0: 16 groups, 8 per half, two distinct bank offsets).
+// With GJKEPA_HULL_AOS the images are 16-byte aligned and, for G < 16, skewed by 4G dwords modulo
+// 64 banks: the G lanes of a group read G consecutive 16-byte vertex records, so the 16-lane groups
+// of a ds_read_b128 (16 / G groups) then cover 256 distinct bytes of banks.
 template <typename L_t, int G> constexpr size_t lds_stride() {
-    size_t dw = (sizeof(L_t) + 7) / 8 * 2;                  // 8-byte aligned, in dwords
-    if (GJKEPA_LDS_SKEW && G < 32)
-        while (dw % 32 != (size_t)G) dw += 2;
-    return dw * 4;
+    if constexpr (GJKEPA_HULL_AOS) {
+        size_t dw = (sizeof(L_t) + 15) / 16 * 4;            // 16-byte aligned, in dwords
+        if (GJKEPA_LDS_SKEW && G < 16)
+            while (dw % 64 != (size_t)(4 * G)) dw += 4;
+        return dw * 4;
+    } else {
+        size_t dw = (sizeof(L_t) + 7) / 8 * 2;              // 8-byte aligned, in dwords
+        if (GJKEPA_LDS_SKEW && G < 32)
+            while (dw % 32 != (size_t)G) dw += 2;
+        return dw * 4;
+    }
 }
 
 template <typename T, typename TH, int G, int K, int VC, int FC, int LH> struct Ctx {
@@ -162,14 +180,35 @@ template <typename T, typename TH, int G, int K, int VC, int FC, int LH> struct 
     T ax[kRegHull ? K : 1], ay[kRegHull ? K : 1], az[kRegHull ? K : 1];
     T bx[kRegHull ? K : 1], by[kRegHull ? K : 1], bz[kRegHull ? K : 1];
     int na, nb;
-    DEV T Ax(int k) const { if constexpr (kRegHull) return ax[k]; else return (T)L.hx[0][k * G + g.gl]; }
-    DEV T Ay(int k) const { if constexpr (kRegHull) return ay[k]; else return (T)L.hy[0][k * G + g.gl]; }
-    DEV T Az(int k) const { if constexpr (kRegHull) return az[k]; else return (T)L.hz[0][k * G + g.gl]; }
-    DEV T Bx(int k) const { if constexpr (kRegHull) return bx[k]; else return (T)L.hx[1][k * G + g.gl]; }
-    DEV T By(int k) const { if constexpr (kRegHull) return by[k]; else return (T)L.hy[1][k * G + g.gl]; }
-    DEV T Bz(int k) const { if constexpr (kRegHull) return bz[k]; else return (T)L.hz[1][k * G + g.gl]; }
-    DEV V3<T> A(int i) const { return vmk<T>((T)L.hx[0][i], (T)L.hy[0][i], (T)L.hz[0][i]); }
-    DEV V3<T> B(int i) const { return vmk<T>((T)L.hx[1][i], (T)L.hy[1][i], (T)L.hz[1][i]); }
+    float vmax_a = 0, vmax_b = 0;   // largest |coordinate| of each hull (fp32 support screen)
+#if GJKEPA_HULL_AOS
+    // vertex i of hull h in storage precision, fetched whole (one 16-byte LDS read for fp32)
+    DEV V3<TH> raw(int h, int i) const {
+        if constexpr (sizeof(TH) == 4) {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            const f4 v = *reinterpret_cast<const f4*>(&L.hv[h][i]);
+            return vmk<TH>(v.x, v.y, v.z);
+        } else {
+            const HV<TH> v = L.hv[h][i];
+            return vmk<TH>(v.x, v.y, v.z);
+        }
+    }
+    DEV TH rawc(int h, int i, int ax) const { return ax == 0 ? L.hv[h][i].x : ax == 1 ? L.hv[h][i].y : L.hv[h][i].z; }
+#else
+    DEV V3<TH> raw(int h, int i) const { return vmk<TH>(L.hx[h][i], L.hy[h][i], L.hz[h][i]); }
+    DEV TH rawc(int h, int i, int ax) const { return ax == 0 ? L.hx[h][i] : ax == 1 ? L.hy[h][i] : L.hz[h][i]; }
+#endif
+    DEV V3<T> A(int i) const { const V3<TH> v = raw(0, i); return vmk<T>((T)v.x, (T)v.y, (T)v.z); }
+    DEV V3<T> B(int i) const { const V3<TH> v = raw(1, i); return vmk<T>((T)v.x, (T)v.y, (T)v.z); }
+    // this lane's k-th vertex (k*G + gl) of hull A / B as a whole vector
+    DEV V3<T> AV(int k) const { if constexpr (kRegHull) return vmk<T>(ax[k], ay[k], az[k]); else return A(k * G + g.gl); }
+    DEV V3<T> BV(int k) const { if constexpr (kRegHull) return vmk<T>(bx[k], by[k], bz[k]); else return B(k * G + g.gl); }
+    DEV T Ax(int k) const { if constexpr (kRegHull) return ax[k]; else return (T)rawc(0, k * G + g.gl, 0); }
+    DEV T Ay(int k) const { if constexpr (kRegHull) return ay[k]; else return (T)rawc(0, k * G + g.gl, 1); }
+    DEV T Az(int k) const { if constexpr (kRegHull) return az[k]; else return (T)rawc(0, k * G + g.gl, 2); }
+    DEV T Bx(int k) const { if constexpr (kRegHull) return bx[k]; else return (T)rawc(1, k * G + g.gl, 0); }
+    DEV T By(int k) const { if constexpr (kRegHull) return by[k]; else return (T)rawc(1, k * G + g.gl, 1); }
+    DEV T Bz(int k) const { if constexpr (kRegHull) return bz[k]; else return (T)rawc(1, k * G + g.gl, 2); }
     DEV V3<T> vert(int i) const { return vmk<T>(L.u.e.vx[i], L.u.e.vy[i], L.u.e.vz[i]); }
 };
 #define CTX_T template <typename T, typename TH, int G, int K, int VC, int FC, int LH>
@@ -179,14 +218,69 @@ template <typename T, typename TH, int G, int K, int VC, int FC, int LH> struct 
 // indices: argmax_i d.a_i (first), argmax_j (-d).b_j (first); -dot(d,b) == dot(-d,b) bit for bit.
 // The group max of the values is reduced alone; the lowest index holding it is then found with
 // one ballot per register slot k (index k*G + lane: lower k first, then lower lane).
+// fp32-screened support (GJKEPA_SCREEN_MIN_K; fp64 compute over fp32-stored hulls): the dots are
+// first taken in fp32 from the stored coordinates (no conversions, half-rate-free arithmetic).  With
+// S = |d|_1 max|v| (vmax: the hull's largest |coordinate|), every fp32 dot is within 4.0001 * 2^-24 S
+// of the exact dot and every fp64 dot within 2^-51 S, so a vertex whose fp32 dot is below the fp32
+// maximum by more than 2E = 2^-18 |d|_1 vmax (E = 32 * 2^-24 * S: 8x margin) has a strictly smaller
+// fp64 dot than the fp32 maximum's vertex and cannot be the fp64 argmax.  Only the remaining
+// candidates (usually one per group) get the fp64 dot, in this lane's index order, and the group
+// takes the largest value, lowest index on ties: the same index as the plain scan.  A non-finite
+// screen (overflow, NaN direction) makes every vertex a candidate.
+template <int K> struct ScreenOn {
+    static constexpr bool value = GJKEPA_SCREEN_MIN_K > 0 && K >= GJKEPA_SCREEN_MIN_K;
+};
+CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) {
+    const float fx = (float)d.x, fy = (float)d.y, fz = (float)d.z;
+    const float sg = h ? -1.0f : 1.0f;
+    const int n = h ? c.nb : c.na;
+    float sv[K];
+    float m = -FLT_MAX;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + c.g.gl;
+        const V3<TH> v = c.raw(h, i < n ? i : 0);
+        const float t = sg * fmaf(fz, v.z, fmaf(fy, v.y, fx * v.x));
+        sv[k] = i < n ? t : -FLT_MAX;
+        m = fmaxf(m, sv[k]);
+    }
+    m = gmax<G>(m);
+    const float thr = m - 0x1p-18f * ((fabsf(fx) + fabsf(fy) + fabsf(fz)) * vmax);
+    uint32_t cand = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + c.g.gl;
+        if (i < n && !(sv[k] < thr)) cand |= 1u << k;      // NaN threshold or value: candidate
+    }
+    T best = -Tol<T>::BIG;
+    int bi = 0x7FFFFFFF;
+    while (cand) {                                          // this lane's candidates in index order
+        const int k = __builtin_ctz(cand);
+        cand &= cand - 1u;
+        const int i = k * G + c.g.gl;
+        const V3<T> v = h ? c.B(i) : c.A(i);
+        const T t = h ? -(d.x * v.x + d.y * v.y + d.z * v.z) : d.x * v.x + d.y * v.y + d.z * v.z;
+        if (t > best) { best = t; bi = i; }
+    }
+    const T vm = gmax<G>(best);
+    const int key = gmin<G>(best == vm ? bi : 0x7FFFFFFF);
+    out = c.g.uni(key == 0x7FFFFFFF ? 0 : key);
+}
+
 CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
+    if constexpr (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) {
+        screened_idx(c, d, 0, c.vmax_a, ia);
+        screened_idx(c, d, 1, c.vmax_b, ib);
+        return;
+    }
     T ta[K], tb[K];
     T va = -Tol<T>::BIG, vb = -Tol<T>::BIG;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
-        ta[k] = i < c.na ? d.x * c.Ax(k) + d.y * c.Ay(k) + d.z * c.Az(k) : -Tol<T>::BIG;
-        tb[k] = i < c.nb ? -(d.x * c.Bx(k) + d.y * c.By(k) + d.z * c.Bz(k)) : -Tol<T>::BIG;
+        const V3<T> a = c.AV(k), b = c.BV(k);
+        ta[k] = i < c.na ? d.x * a.x + d.y * a.y + d.z * a.z : -Tol<T>::BIG;
+        tb[k] = i < c.nb ? -(d.x * b.x + d.y * b.y + d.z * b.z) : -Tol<T>::BIG;
         va = ta[k] > va ? ta[k] : va;
         vb = tb[k] > vb ? tb[k] : vb;
     }
@@ -300,7 +394,7 @@ constexpr uint32_t kEmpty = 0x80000000u;
 
 template <typename T, int R> struct Faces {
     T nx[R], ny[R], nz[R];     // unit normal
-    T d[R];                    // |plane distance of the origin|
+    T d[R];                    // DIST_PF_SIGN(O, face) (signed: the EPA distance is |d|, the plane offset -d)
     uint32_t fv[R];            // v0 | v1 << 8 | v2 << 16, kEmpty = free slot
     uint32_t key[R];           // creation order
 };
@@ -326,8 +420,8 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         bool vis = false;
         live[r] = __ballot(valid) != 0;
         if (live[r]) {
-            const V3<T> a = c.vert(valid ? (int)(F.fv[r] & 0xffu) : 0), n = vmk<T>(F.nx[r], F.ny[r], F.nz[r]);
-            vis = valid && dot(vsub(p, a), n) > Tol<T>::HULL;
+            // signed distance of p above the face plane: n.p - n.v0 = dot(p, n) + DIST_PF_SIGN(O, face)
+            vis = valid && dot(p, vmk<T>(F.nx[r], F.ny[r], F.nz[r])) + F.d[r] > Tol<T>::HULL;
         }
         vm[r] = c.g.ballot(vis);
         nvis += popc(vm[r]);
@@ -403,7 +497,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int f = r * G + gl;
-            if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
+            if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : fabs(F.d[r]);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -433,7 +527,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             const V3<T> U = c.vert(u), W = c.vert(w);
             const V3<T> n = uninml(U, W, P);
             bad = bad || is_zero_nml(n);
-            const T dd = fabs(dot(vsub(zero3<T>(), U), n));
+            const T dd = dot(vsub(zero3<T>(), U), n);
             const uint32_t fv = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16), kk = E.x.h.hork[h];
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -490,7 +584,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             const V3<T> n = uninml(U, W, P);
             bad = bad || is_zero_nml(n);
             E.x.h.sn[gl][0] = n.x; E.x.h.sn[gl][1] = n.y; E.x.h.sn[gl][2] = n.z;
-            E.x.h.sn[gl][3] = fabs(dot(vsub(zero3<T>(), U), n));
+            E.x.h.sn[gl][3] = dot(vsub(zero3<T>(), U), n);
             E.x.h.sv[gl] = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
             E.x.h.sk[gl] = E.x.h.hork[h];
         }
@@ -556,7 +650,7 @@ CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, 
         const V3<T> n = uninml(Pa, Pb, Pd);
         bad = is_zero_nml(n);
         F.nx[0] = n.x; F.ny[0] = n.y; F.nz[0] = n.z;
-        F.d[0] = fabs(dot(vsub(zero3<T>(), Pa), n));
+        F.d[0] = dot(vsub(zero3<T>(), Pa), n);
         F.fv[0] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)d << 16);
         F.key[0] = (uint32_t)gl;
     }
@@ -576,7 +670,7 @@ CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, 
 // MINLOC of the face distances (first in list order = lowest key): value-only group min, then
 // the key breaks a tie between lanes.  The winner's normal, first vertex and distance are
 // broadcast through the group's LDS slot.
-CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, V3<T>& a) {
+CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& neg, int& av) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     T v = Tol<T>::BIG;
@@ -586,7 +680,8 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, V3<T>& a
     for (int r = 0; r < R; ++r) {
         const bool valid = !(F.fv[r] & kEmpty);
         if (!__ballot(valid)) continue;
-        if (valid && (F.d[r] < v || (F.d[r] == v && F.key[r] < kk))) { v = F.d[r]; kk = F.key[r]; rr = r; }
+        const T ad = fabs(F.d[r]);
+        if (valid && (ad < v || (ad == v && F.key[r] < kk))) { v = ad; kk = F.key[r]; rr = r; }
     }
     const T vmin = gmin<G>(v);
     const bool tie = rr >= 0 && v == vmin;
@@ -600,13 +695,15 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, V3<T>& a
         for (int r = 0; r < R; ++r)
             if (rr == r) {
                 E.best[0] = F.nx[r]; E.best[1] = F.ny[r]; E.best[2] = F.nz[r];
-                E.bestv = F.fv[r] & 0xffu;
+                E.bestv = (F.fv[r] & 0xffu) | (F.d[r] < T(0) ? 0x80000000u : 0u);
             }
     }
     __builtin_amdgcn_wave_barrier();
     dmin = vmin;
     n = vmk<T>(E.best[0], E.best[1], E.best[2]);
-    a = c.vert((int)E.bestv);
+    const uint32_t bv = E.bestv;
+    neg = (bv >> 31) != 0;
+    av = (int)(bv & 0xffu);
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -620,7 +717,7 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F, int hw) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int f = r * G + gl;
-        if (f < FC) E.x.s.cur[f] = (F.fv[r] & kEmpty) ? qnan<T>() : F.d[r];
+        if (f < FC) E.x.s.cur[f] = (F.fv[r] & kEmpty) ? qnan<T>() : fabs(F.d[r]);
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -698,7 +795,9 @@ template <typename T, int R> struct EpaState {
     int nv, hw, nf, F1, iters;
     uint32_t kbase;
     T minv;
-    V3<T> dir, a1;                 // MINLOC face of the current polytope (normal, first vertex)
+    V3<T> dir;                     // MINLOC face of the current polytope: normal,
+    bool neg;                      //   DIST_PF_SIGN(O, face) < 0,
+    int av;                        //   first vertex id
     bool unchanged;
 };
 #define EPAST_T EpaState<T, (FC + G - 1) / G>
@@ -769,9 +868,11 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     const V3<T> O = zero3<T>();
     const int gl = c.g.gl;
     const int F2 = S.nf;                                      // :956-969
-    face_argmin(c, S.F, S.minv, S.dir, S.a1);
+    face_argmin(c, S.F, S.minv, S.dir, S.neg, S.av);
+    // dot(a1 - O, n) is -DIST_PF_SIGN(O, face) (exact negation; a zero's sign never matters here):
+    // negative iff the face's signed distance is positive
     V3<T> dir2 = S.dir;
-    if (c.g.unib(dot(vsub(S.a1, O), dir2) < T(0))) dir2 = vneg(dir2);
+    if (c.g.unib(!S.neg && S.minv > T(0))) dir2 = vneg(dir2);
     bool stop;                                                // :972-1015
     if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F, S.hw);   // unchanged hull: identical sorted lists
     else stop = S.F1 > F2;
@@ -782,8 +883,9 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     if (S.iters > 99) return GJKEPA_STATUS_EPA_MAXITER;
     S.F1 = S.nf;
     V3<T> dir = S.dir;
-    T dt = dot(vsub(S.a1, O), dir);
-    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) dt = dot(vsub(S.a1, polytope_centroid(c, S.F, S.F1, S.hw)), dir);   // :905-908
+    T dt = S.neg ? S.minv : -S.minv;                           // dot(a1 - O, dir)
+    if (c.g.unib(S.minv < Tol<T>::ZO))                        // :905-908
+        dt = dot(vsub(c.vert(S.av), polytope_centroid(c, S.F, S.F1, S.hw)), dir);
     if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
     GK_STAMP(SE_DIR);
     const V3<T> sp = support(c, dir);                          // :914
@@ -793,7 +895,7 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int f = r * G + gl;
-            if (f < FC) E.dsv[f] = (S.F.fv[r] & kEmpty) ? qnan<T>() : S.F.d[r];
+            if (f < FC) E.dsv[f] = (S.F.fv[r] & kEmpty) ? qnan<T>() : fabs(S.F.d[r]);
         }
     }
     bool ch1 = false, ch2 = false;
@@ -835,7 +937,8 @@ CTX_T DEV T hull_dot_max(CTX& c, int side, V3<T> n) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         int i = k * G + c.g.gl;
-        T t = side ? n.x * c.Bx(k) + n.y * c.By(k) + n.z * c.Bz(k) : n.x * c.Ax(k) + n.y * c.Ay(k) + n.z * c.Az(k);
+        const V3<T> p = side ? c.BV(k) : c.AV(k);
+        T t = n.x * p.x + n.y * p.y + n.z * p.z;
         if (i < (side ? c.nb : c.na) && t > mx) mx = t;
     }
     return gmax<G>(mx);
@@ -847,7 +950,8 @@ CTX_T DEV int hull_band_set(CTX& c, int side, V3<T> n, T mx, T band, bool store)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         int i = k * G + c.g.gl;
-        T px = side ? c.Bx(k) : c.Ax(k), py = side ? c.By(k) : c.Ay(k), pz = side ? c.Bz(k) : c.Az(k);
+        const V3<T> p = side ? c.BV(k) : c.AV(k);
+        T px = p.x, py = p.y, pz = p.z;
         T t = n.x * px + n.y * py + n.z * pz;
         bool in = i < (side ? c.nb : c.na) && t > mx - band;
         uint64_t m = c.g.ballot(in);
@@ -1102,7 +1206,7 @@ CTX_T DEV int contact_v3(CTX& c, V3<T> n, V3<T>& res, V3<T>& nnew) {
     }
     if (idx < 0) return GJKEPA_STATUS_DEGENERATE;
     T sz = 0;
-    for (int i = 0; i < c.na; ++i) sz += (T)c.L.hz[0][i];
+    for (int i = 0; i < c.na; ++i) sz += (T)c.rawc(0, i, 2);
     res = c.B(idx);
     res.z = sz / (T)(float)c.na;
     const V3<T> q = vmk<T>(n.x, n.y, T(0));
@@ -1216,18 +1320,24 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
             const int j = j0 + gl;
             if (j < 6) {
                 const int h = j / 3, ax = j - 3 * (j / 3);
+#if GJKEPA_HULL_AOS
+                const TH* col = &L.hv[h][0].x + ax;  // coordinate ax of vertex i at col[4 i]
+                constexpr int CS = 4;
+#else
                 const TH* col = ax == 0 ? L.hx[h] : ax == 1 ? L.hy[h] : L.hz[h];
+                constexpr int CS = 1;
+#endif
                 const int n = h ? c.nb : c.na;
                 T sum = 0;
                 int i = 0;
                 for (; i + 8 <= n; i += 8) {         // loads batched ahead of the in-order adds
                     TH v[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = col[i + u];
+                    for (int u = 0; u < 8; ++u) v[u] = col[CS * (i + u)];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) sum += (T)v[u];
                 }
-                for (; i < n; ++i) sum += (T)col[i];
+                for (; i < n; ++i) sum += (T)col[CS * i];
                 L.u.g.l1[j] = sum / (T)n;
             }
         }
@@ -1239,10 +1349,10 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             int i = k * G + gl;
-            const V3<T> da = vsub(vmk<T>(c.Ax(k), c.Ay(k), c.Az(k)), m1);
+            const V3<T> da = vsub(c.AV(k), m1);
             const T ta = da.x * da.x + da.y * da.y + da.z * da.z;
             if (i < c.na && ta > r1) r1 = ta;
-            const V3<T> db = vsub(vmk<T>(c.Bx(k), c.By(k), c.Bz(k)), m2);
+            const V3<T> db = vsub(c.BV(k), m2);
             const T tb = db.x * db.x + db.y * db.y + db.z * db.z;
             if (i < c.nb && tb > r2) r2 = tb;
         }
@@ -1261,8 +1371,9 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int i = k * G + gl;
-                const T ta = d.x * c.Ax(k) + d.y * c.Ay(k) + d.z * c.Az(k);
-                const T tb = d.x * c.Bx(k) + d.y * c.By(k) + d.z * c.Bz(k);
+                const V3<T> pa = c.AV(k), pb = c.BV(k);
+                const T ta = d.x * pa.x + d.y * pa.y + d.z * pa.z;
+                const T tb = d.x * pb.x + d.y * pb.y + d.z * pb.z;
                 if (i < c.na && ta > amax) amax = ta;
                 if (i < c.nb && tb < bmin) bmin = tb;
             }
@@ -1400,6 +1511,8 @@ CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* 
 CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restrict__ pb) {
     const int gl = c.g.gl;
     bool nonfinite = false;
+    constexpr bool kScreen = ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4;
+    float ma = 0.0f, mb = 0.0f;     // largest |coordinate| (support screen bound; padding lanes hold 0)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + gl;
@@ -1408,12 +1521,25 @@ CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restric
         if (i < c.nb) { bx = pb[i]; by = pb[c.nb + i]; bz = pb[2 * c.nb + i]; }
         nonfinite = nonfinite || !isfinite(ax) || !isfinite(ay) || !isfinite(az) || !isfinite(bx) ||
                     !isfinite(by) || !isfinite(bz);
+        if constexpr (kScreen) {
+            ma = fmaxf(ma, fmaxf(fabsf((float)ax), fmaxf(fabsf((float)ay), fabsf((float)az))));
+            mb = fmaxf(mb, fmaxf(fabsf((float)bx), fmaxf(fabsf((float)by), fabsf((float)bz))));
+        }
         if constexpr (CTX::kRegHull) {
             c.ax[k] = (T)ax; c.ay[k] = (T)ay; c.az[k] = (T)az;
             c.bx[k] = (T)bx; c.by[k] = (T)by; c.bz[k] = (T)bz;
         }
+#if GJKEPA_HULL_AOS
+        c.L.hv[0][i] = HV<TH>{ax, ay, az, TH(0)};
+        c.L.hv[1][i] = HV<TH>{bx, by, bz, TH(0)};
+#else
         c.L.hx[0][i] = ax; c.L.hy[0][i] = ay; c.L.hz[0][i] = az;
         c.L.hx[1][i] = bx; c.L.hy[1][i] = by; c.L.hz[1][i] = bz;
+#endif
+    }
+    if constexpr (kScreen) {
+        c.vmax_a = gmax<G>(ma);
+        c.vmax_b = gmax<G>(mb);
     }
     __builtin_amdgcn_wave_barrier();
     return c.g.any(nonfinite);

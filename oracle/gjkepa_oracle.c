@@ -216,7 +216,7 @@ static void update_simplex(const hull_t* a, const hull_t* b, v3* S) {
 }
 
 /* ---- re-supplied hull (GCLIB_QuickHull / GCLIB_DeHull semantics, see file header) ----------- */
-typedef struct { int v[3]; v3 n; double d; } face_t;
+typedef struct { int v[3]; v3 n; double sd, d; } face_t;   /* sd = DIST_PF_SIGN(O, face), d = |sd| */
 typedef struct {
     v3 vert[OVCAP];
     int nv;
@@ -228,23 +228,27 @@ typedef struct {
     double d1[OFCAP], d2[OFCAP];
 } hullbuf;
 
-/* face record: plane normal UNINML of the stored (outward) order, |DIST_PF_SIGN(O, face)| */
+/* face record: plane normal UNINML of the stored (outward) order, DIST_PF_SIGN(O, face) and its
+ * absolute value (the EPA face distance) */
 static int make_face(const hullbuf* H, int a, int b, int c, face_t* f) {
     f->v[0] = a; f->v[1] = b; f->v[2] = c;
     v3 n = uninml(H->vert[a], H->vert[b], H->vert[c]);
     if (is_zero_nml(n)) return GJKEPA_STATUS_DEGENERATE;   /* :958-960 -> :1369-1373 */
     f->n = n;
-    f->d = fabs(dot(vsub(ORIGIN, H->vert[a]), n));
+    f->sd = dot(vsub(ORIGIN, H->vert[a]), n);
+    f->d = fabs(f->sd);
     return 0;
 }
 
 /* Add vertex index k (already in H->vert) to the hull: faces with signed distance > HULL_EPS are
- * removed, the horizon is coned to k.  *changed = 0 when k is inside / on the hull. */
+ * removed, the horizon is coned to k.  *changed = 0 when k is inside / on the hull.  The signed
+ * distance of p from a face's plane is n.p - n.v0 = dot(p, n) + DIST_PF_SIGN(O, face): the plane
+ * offset is the face's own origin distance, so the test needs no vertex coordinates. */
 static int hull_add(hullbuf* H, int k, int* changed) {
     v3 p = H->vert[k];
     int nvis = 0;
     for (int f = 0; f < H->nf; ++f) {
-        H->vis[f] = dot(vsub(p, H->vert[H->f[f].v[0]]), H->f[f].n) > HULL_EPS;
+        H->vis[f] = dot(p, H->f[f].n) + H->f[f].sd > HULL_EPS;
         nvis += H->vis[f];
     }
     *changed = nvis > 0;
