@@ -814,18 +814,22 @@ CTX_T DEV int epa_begin(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> 
         if (f < FC) E.dsv[f] = qnan<T>();
     }
     S.nv = 0; S.hw = 0; S.nf = 0; S.kbase = 0; S.iters = 1; S.F1 = 4; S.unchanged = false;
-    // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN
-    const V3<T> f0 = uninml(s0, s1, s2), f1 = uninml(s0, s2, s3), f2 = uninml(s0, s1, s3), f3 = uninml(s1, s2, s3);
-    if (c.g.unib(is_zero_nml(f0) || is_zero_nml(f1) || is_zero_nml(f2) || is_zero_nml(f3)))
-        return GJKEPA_STATUS_DEGENERATE;
-    const T d0 = fabs(dot(vsub(O, s0), f0)), d1 = fabs(dot(vsub(O, s0), f1));
-    const T d2 = fabs(dot(vsub(O, s0), f2)), d3 = fabs(dot(vsub(O, s1), f3));
-    T minv = d0;
-    V3<T> dir = f0, a1 = s0;
-    if (d1 < minv) { minv = d1; dir = f1; a1 = s0; }
-    if (d2 < minv) { minv = d2; dir = f2; a1 = s0; }
-    if (d3 < minv) { minv = d3; dir = f3; a1 = s1; }
-    if (gl < 4) E.dsv[gl] = gl == 0 ? d0 : gl == 1 ? d1 : gl == 2 ? d2 : d3;
+    // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293), distances via DIST_PF_SIGN: quad lane q
+    // builds face q (its first vertex is the distance reference), the quad shares the results
+    const int fq = gl & 3;
+    const V3<T> fa = fq == 3 ? s1 : s0, fb = (fq == 0 || fq == 2) ? s1 : s2, fc = fq == 0 ? s2 : s3;
+    const V3<T> nq = uninml(fa, fb, fc);
+    if (c.g.unib(quad_any(is_zero_nml(nq)))) return GJKEPA_STATUS_DEGENERATE;
+    const T dq = fabs(dot(vsub(O, fa), nq));
+    const T d0 = qbcast<0>(dq), d1 = qbcast<1>(dq), d2 = qbcast<2>(dq), d3 = qbcast<3>(dq);
+    T minv = d0;                                              // MINLOC, first index
+    int kmin = 0;
+    if (d1 < minv) { minv = d1; kmin = 1; }
+    if (d2 < minv) { minv = d2; kmin = 2; }
+    if (d3 < minv) { minv = d3; kmin = 3; }
+    V3<T> dir = quad_pick(fq == kmin, nq);
+    const V3<T> a1 = kmin == 3 ? s1 : s0;
+    if (gl < 4) E.dsv[gl] = dq;
     T dt = dot(vsub(a1, O), dir);
     if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
         // SUM over polytope(:,:,k), slot-major over faces: [s0 s0 s0 s1][s1 s2 s1 s2][s2 s3 s3 s3]

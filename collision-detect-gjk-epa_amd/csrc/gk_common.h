@@ -178,6 +178,24 @@ template <int J> DEV double qbcast(double v) {
 }
 template <int J> DEV float qbcast(float v) { return __builtin_bit_cast(float, qb32<J>(__builtin_bit_cast(uint32_t, v))); }
 DEV bool quad_all(bool b) { int x = b; x &= xchg<0>(x); x &= xchg<1>(x); return x != 0; }
+// the value of the one quad lane where `mine` holds, on every lane of the quad (bitwise OR of the
+// quad's masked values: exact, signed zeros included)
+DEV double quad_pick(bool mine, double v) {
+    uint64_t u = mine ? __builtin_bit_cast(uint64_t, v) : 0ull;
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    lo |= xchg32<0>(lo); hi |= xchg32<0>(hi);
+    lo |= xchg32<1>(lo); hi |= xchg32<1>(hi);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+DEV float quad_pick(bool mine, float v) {
+    uint32_t u = mine ? __builtin_bit_cast(uint32_t, v) : 0u;
+    u |= xchg32<0>(u);
+    u |= xchg32<1>(u);
+    return __builtin_bit_cast(float, u);
+}
+template <typename T> DEV V3<T> quad_pick(bool mine, V3<T> v) {
+    return vmk<T>(quad_pick(mine, v.x), quad_pick(mine, v.y), quad_pick(mine, v.z));
+}
 DEV bool quad_any(bool b) { int x = b; x |= xchg<0>(x); x |= xchg<1>(x); return x != 0; }
 
 // group-wide (value, index) argmax / argmin with lowest-index tie break; max
