@@ -15,6 +15,9 @@ Candidates are deterministic (seeded) families of structured and random pairs:
   tiny      the same at 1e-7..1e-3 scale: the absolute 1e-8 collinear exit (:199-201)
   c4        the C4 distribution (8-256 vertices): the 99-iteration EPA cap (:299-302)
   invalid   an empty hull and a 257-vertex hull (BAD_INPUT)
+  scaled    4-12-vertex Gaussian hulls at 1e3..1e8 scale (tools/branch_search.py "big"): the absolute
+            1e-8 exits no longer fire, and GJK's tetrahedron loop cycles (:219-234) or runs into its
+            50-iteration cap (:186); only the pairs taking those two branches are kept
 Each branch keeps its first PER_BRANCH pairs (smallest hulls first within a family).  Records are
 the oracle's for version_ 1, 2, 3 and 4 (4 exercises BAD_VERSION on hits, :336-339).
 
@@ -39,7 +42,7 @@ import oracle  # noqa: E402
 PER_BRANCH = 4
 VERSIONS = (1, 2, 3, 4)
 # reference branches the search does not reach (DESIGN.md §2.1 gives the argument for each)
-UNREACHED = ("LOOP_CAP", "LOOP_CYCLE", "EPA_STOP_SHRINK", "V2_OVERLAP")
+UNREACHED = ("EPA_STOP_SHRINK", "V2_OVERLAP")
 
 
 def box(sx=1.0, sy=1.0, sz=1.0):
@@ -101,6 +104,25 @@ def families():
     yield "c4", [(pool.hull(int(pool.pairs[k, 0])).astype(float), pool.hull(int(pool.pairs[k, 1])).astype(float))
                  for k in range(pool.n_pairs)]
     yield "invalid", [(np.zeros((0, 3)), box()), (box(), rng.normal(size=(257, 3)))]
+    yield "scaled", scaled_loop_pairs()
+
+
+def scaled_loop_pairs(n_total=600000, keep=6):
+    """The first `keep` pairs per branch of tools/branch_search.py's "big" family (seeded) that take
+    GJK's loop cap or cycle exit; screened with the vectorised pool builder, oracle bits only."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import branch_search as bs
+    rng = np.random.default_rng(20261017)
+    want = {oracle.BRANCHES.index("LOOP_CAP"): [], oracle.BRANCHES.index("LOOP_CYCLE"): []}
+    done = 0
+    while done < n_total and any(len(v) < keep for v in want.values()):
+        A, B = bs.fam(rng, "big", 100000)
+        m = oracle.gjkepa_batch_cov(bs.pool_of(A, B), 2, 1.0, 8)[1]
+        for b, lst in want.items():
+            for k in np.nonzero((m >> np.uint64(b)) & np.uint64(1))[0][:keep - len(lst)]:
+                lst.append((A[k], B[k]))
+        done += 100000
+    return [p for lst in want.values() for p in lst]
 
 
 def main():
@@ -132,8 +154,8 @@ def main():
     print("branch_cov", pool.n_pairs, "pairs", os.path.getsize(os.path.join(HERE, "branch_cov.npz")), "bytes")
     hist = histogram_of_fixtures()
     hist["_search"] = {"families": searched, "unreached": list(UNREACHED)}
-    os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "r02", "branch_coverage.json"), "w") as f:
+    os.makedirs(os.path.join(ROOT, "profiles", "r03"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "r03", "branch_coverage.json"), "w") as f:
         json.dump(hist, f, indent=1)
     missing = [n for n in oracle.BRANCHES if hist["branch_cov"][n] == 0]
     print("branches not covered:", missing)

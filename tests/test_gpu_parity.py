@@ -156,14 +156,29 @@ def test_device_api_matches_host_api():
     assert out.cpu().numpy().tobytes() == host.tobytes()
 
 
+def fp32_errors(g, r):
+    """Per-hit errors of fp32-compute records g against fp64 oracle records r (both OK hits):
+    relative depth error and the angle (rad) between the normals."""
+    m = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
+    dr = r["penetration_depth"][m].astype(np.float64)
+    de = np.abs(g["penetration_depth"][m].astype(np.float64) - dr) / np.maximum(np.abs(dr), 1e-9)
+    a = g["collision_normal"][m].astype(np.float64)
+    b = r["collision_normal"][m].astype(np.float64)
+    cosang = np.sum(a * b, axis=1) / np.maximum(np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1), 1e-300)
+    return de, np.arccos(np.clip(cosang, -1.0, 1.0))
+
+
 def test_fp32_tolerance_sweep(orc):
-    """fp32 compute (throughput path): hit flags vs the fp64 oracle, depth/normal error bounds."""
+    """fp32 compute (throughput path): hit flags vs the fp64 oracle, and gates on the depth and
+    normal errors: p99.9 relative depth error < 1e-5 and p99.9 normal angle < 1e-5
+    rad; a pair whose fp32 polytope picks a different near-tied face can be off by more, so the
+    tail is bounded separately (depth 1e-3 relative, angle 0.05 rad)."""
     for name, lo, hi, rmax in [("C2", 32, 32, 2.5), ("C5", 64, 128, 0.3)]:
         pool = gjkepa.synth_pairs(0x6A4B5C1D, 4000, lo, hi, rmax)
         g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F32)
         r = orc.gjkepa_batch(pool, 2, 1.0)
         agree = (g["collision"] == r["collision"]).mean()
         assert agree >= 0.999, (name, agree)
-        m = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
-        d = np.abs(g["penetration_depth"][m] - r["penetration_depth"][m])
-        assert np.quantile(d, 0.99) < 1e-4 and d.max() < 5e-3, (name, np.quantile(d, 0.99), d.max())
+        de, ang = fp32_errors(g, r)
+        assert np.quantile(de, 0.999) < 1e-5 and de.max() < 1e-3, (name, np.quantile(de, 0.999), de.max())
+        assert np.quantile(ang, 0.999) < 1e-5 and ang.max() < 0.05, (name, np.quantile(ang, 0.999), ang.max())
