@@ -233,7 +233,11 @@ def main():
                     valu = {"instr_per_query": round(pj["valu_instr_per_query"], 1),
                             "issue_frac_pmc": round(pj["valu_issue_frac"], 4),
                             "issue_frac_live": round(pj["valu_instr"] * 2.0 / (1024 * kern_ms * 1e-3 * 2.4e9), 4),
-                            "note": "SQ_INSTS_VALU priced at the 2-cycle wave64 issue slot vs 1024 SIMDs x kernel time x 2.4 GHz"}
+                            "busy_frac_pmc": round(pj["valu_busy_frac"], 4) if pj.get("valu_busy_frac") else None,
+                            "traffic_raw_fetch": pj.get("fetch_bytes_raw"),
+                            "note": "issue_frac: SQ_INSTS_VALU at the 2-cycle wave64 slot vs 1024 SIMDs x kernel time x "
+                                    "2.4 GHz (fp64 ops take 4: a lower bound); busy_frac: SQ_ACTIVE_INST_VALU (quad-cycles "
+                                    "x 4) over the same, the VALU-busy share"}
         except Exception:
             traffic, valu, pmc_src = None, None, None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -136,7 +136,10 @@
 #define GJKEPA_C1_K 4
 #endif
 #ifndef GJKEPA_C1_MINW
-#define GJKEPA_C1_MINW 1
+#define GJKEPA_C1_MINW 2        // keeps the LDS-hull contact tier at <= 256 VGPRs (2 waves/SIMD)
+#endif
+#ifndef GJKEPA_EPA_SEED
+#define GJKEPA_EPA_SEED 1           // refill tiers: a fresh pair's iteration 1 joins the common support step (epa_seed)
 #endif
 #ifndef GJKEPA_EPA_PLACE
 #define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
@@ -183,10 +186,10 @@
 #define GJKEPA_E4_LH 0
 #endif
 #ifndef GJKEPA_C0_LH
-#define GJKEPA_C0_LH 0
+#define GJKEPA_C0_LH 1             // contact features read the hull from LDS (A/B r3: C4 +5% with the one-pass dots)
 #endif
 #ifndef GJKEPA_C1_LH
-#define GJKEPA_C1_LH 0
+#define GJKEPA_C1_LH 1
 #endif
 #ifndef GJKEPA_CONTACT_OVERLAP
 #define GJKEPA_CONTACT_OVERLAP 1    // each EPA tier's contact pass on a second stream, overlapping the later EPA tiers

@@ -267,13 +267,15 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
     out = c.g.uni(key == 0x7FFFFFFF ? 0 : key);
 }
 
-CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
-    if constexpr (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) {
-        screened_idx(c, d, 0, c.vmax_a, ia);
-        screened_idx(c, d, 1, c.vmax_b, ib);
-        return;
-    }
-    T ta[K], tb[K];
+// This lane's dots with one direction d over both hulls: t[0][k] = d.a_(kG+gl), t[1][k] = -(d.b_(kG+gl))
+// (= (-d).b bit for bit up to a zero's sign), -BIG past the hull, and the group maxima m[0], m[1]:
+// get_nearest_points' argmax values, and get_info_collisionType's / the contact points' HUGE-start
+// max scans (:381, :401, :471-472) for the same direction.
+template <typename T, int K> struct DotSet { T t[2][K]; T m[2]; };
+
+CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int& ib) {
+    T (&ta)[K] = D.t[0];
+    T (&tb)[K] = D.t[1];
     T va = -Tol<T>::BIG, vb = -Tol<T>::BIG;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -297,6 +299,18 @@ CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
     }
     ia = c.g.uni(xa < 0 ? 0 : xa);
     ib = c.g.uni(xb < 0 ? 0 : xb);
+    D.m[0] = va;
+    D.m[1] = vb;
+}
+
+CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
+    if constexpr (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) {
+        screened_idx(c, d, 0, c.vmax_a, ia);
+        screened_idx(c, d, 1, c.vmax_b, ib);
+        return;
+    }
+    DotSet<T, K> D;
+    support_dots(c, d, D, ia, ib);
 }
 CTX_T DEV V3<T> support(const CTX& c, V3<T> d) {
     int ia, ib;
@@ -864,13 +878,93 @@ CTX_T DEV int epa_begin(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> 
     return hull_build(c, S.F, S.kbase, S.hw, S.nv, S.nf, m);
 }
 
-// Closes iteration S.iters; if EPA goes on, runs the next iteration.  ST_CONT, 0 (depth and
-// normal set) or an error status / ST_DEFER.
-CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
+// EPA iteration 1 up to the support step, for the usual case where hull_build's first tetrahedron is
+// the GJK simplex itself (four distinct points, non-degenerate at the hull epsilon): the seed soup's
+// MINLOC and orientation as in epa_begin (direction in S.dir), the tetrahedron's faces wound outward
+// as hull_build does (slots / keys 0..3) and its points as vertices 0..3.  epa_grow(first = true) then
+// adds the support point(s) as hull_build adds them, in the same pass as the other groups' steps.
+// ST_FALLBACK: the tetrahedron is not the simplex (duplicate or near-degenerate points): epa_begin.
+constexpr int ST_FALLBACK = 102;
+CTX_T DEV int epa_seed(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const V3<T> O = zero3<T>();
     const int gl = c.g.gl;
+    // hull_build's tetrahedron search (first non-degenerate one in list order) must give (0, 1, 2, 3)
+    const bool distinct = !veq(s1, s0) && !veq(s2, s0) && !veq(s2, s1) && !veq(s3, s0) && !veq(s3, s1) && !veq(s3, s2);
+    if (!c.g.unib(distinct)) return ST_FALLBACK;
+    const V3<T> e1 = vsub(s1, s0);
+    const T l1 = norm2(e1);
+    if (!c.g.unib(l1 > Tol<T>::HULL)) return ST_FALLBACK;
+    const V3<T> c2 = cross(e1, vsub(s2, s0));
+    if (!c.g.unib(norm2(c2) / l1 > Tol<T>::HULL)) return ST_FALLBACK;
+    const V3<T> pn = utzvec(c2);
+    if (!c.g.unib(fabs(dot(vsub(s3, s0), pn)) > Tol<T>::HULL)) return ST_FALLBACK;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        S.F.fv[r] = kEmpty;
+        const int f = r * G + gl;
+        if (f < FC) E.dsv[f] = qnan<T>();
+    }
+    S.iters = 1; S.F1 = 4; S.unchanged = false;
+    // seed soup [1,2,3],[1,3,4],[1,2,4],[2,3,4] (:279-293) on the quad lanes, as in epa_begin
+    const int fq = gl & 3;
+    const V3<T> fa = fq == 3 ? s1 : s0, fb = (fq == 0 || fq == 2) ? s1 : s2, fc = fq == 0 ? s2 : s3;
+    const V3<T> nq = uninml(fa, fb, fc);
+    if (c.g.unib(quad_any(is_zero_nml(nq)))) return GJKEPA_STATUS_DEGENERATE;
+    const T dq = fabs(dot(vsub(O, fa), nq));
+    const T d0 = qbcast<0>(dq), d1 = qbcast<1>(dq), d2 = qbcast<2>(dq), d3 = qbcast<3>(dq);
+    T minv = d0;                                              // MINLOC, first index
+    int kmin = 0;
+    if (d1 < minv) { minv = d1; kmin = 1; }
+    if (d2 < minv) { minv = d2; kmin = 2; }
+    if (d3 < minv) { minv = d3; kmin = 3; }
+    V3<T> dir = quad_pick(fq == kmin, nq);
+    const V3<T> a1 = kmin == 3 ? s1 : s0;
+    if (gl < 4) E.dsv[gl] = dq;
+    T dt = dot(vsub(a1, O), dir);
+    if (c.g.unib(fabs(dt) < Tol<T>::ZO)) {                    // :905-908 polytope centroid
+        const T sx = ((((((((((s0.x + s0.x) + s0.x) + s1.x) + s1.x) + s2.x) + s1.x) + s2.x) + s2.x) + s3.x) + s3.x) + s3.x;
+        const T sy = ((((((((((s0.y + s0.y) + s0.y) + s1.y) + s1.y) + s2.y) + s1.y) + s2.y) + s2.y) + s3.y) + s3.y) + s3.y;
+        const T sz = ((((((((((s0.z + s0.z) + s0.z) + s1.z) + s1.z) + s2.z) + s1.z) + s2.z) + s2.z) + s3.z) + s3.z) + s3.z;
+        const T cnt = (T)12;
+        dt = dot(vsub(a1, vmk<T>(sx / cnt, sy / cnt, sz / cnt)), dir);
+    }
+    if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+    S.dir = dir;                                              // epa_grow's support direction
+    S.minv = minv;                                            // epa_grow's two-point test (:935)
+    // vertices 0..3 and the tetrahedron's faces wound outward (hull_build with i1, i2, i3 = 1, 2, 3)
+    if (gl < 4) {
+        const V3<T> q = gl == 0 ? s0 : gl == 1 ? s1 : gl == 2 ? s2 : s3;
+        E.vx[gl] = q.x; E.vy[gl] = q.y; E.vz[gl] = q.z;
+    }
+    const V3<T> cen = centroid4(s0, s1, s2, s3);
+    bool bad = false;
+    if (gl < 4) {
+        int a = gl == 3 ? 1 : 0, b = (gl == 0 || gl == 2) ? 1 : 2, d = gl == 0 ? 2 : 3;
+        const V3<T> Pa = vsel(gl == 3, s1, s0);
+        V3<T> Pb = vsel(gl == 0 || gl == 2, s1, s2);
+        V3<T> Pd = vsel(gl == 0, s2, s3);
+        const V3<T> n0 = cross(vsub(Pb, Pa), vsub(Pd, Pb));
+        if (dot(n0, vsub(Pa, cen)) < T(0)) { int t = b; b = d; d = t; const V3<T> q = Pb; Pb = Pd; Pd = q; }
+        const V3<T> n = uninml(Pa, Pb, Pd);
+        bad = is_zero_nml(n);
+        S.F.nx[0] = n.x; S.F.ny[0] = n.y; S.F.nz[0] = n.z;
+        S.F.d[0] = dot(vsub(zero3<T>(), Pa), n);
+        S.F.fv[0] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)d << 16);
+        S.F.key[0] = (uint32_t)gl;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (c.g.any(bad)) return GJKEPA_STATUS_DEGENERATE;
+    S.nv = 4; S.nf = 4; S.kbase = 4; S.hw = 4;
+    GK_STAMP(SE_IT1);
+    return 0;
+}
+
+// Closes iteration S.iters (MINLOC of the polytope, termination :956-1015); if EPA goes on, the
+// next iteration's direction (:888-910) replaces S.dir.  ST_CONT, 0 (depth and normal set) or a status.
+CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
+    const V3<T> O = zero3<T>();
     const int F2 = S.nf;                                      // :956-969
     face_argmin(c, S.F, S.minv, S.dir, S.neg, S.av);
     // dot(a1 - O, n) is -DIST_PF_SIGN(O, face) (exact negation; a zero's sign never matters here):
@@ -886,16 +980,27 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     S.iters = S.iters + 1;
     if (S.iters > 99) return GJKEPA_STATUS_EPA_MAXITER;
     S.F1 = S.nf;
-    V3<T> dir = S.dir;
     T dt = S.neg ? S.minv : -S.minv;                           // dot(a1 - O, dir)
     if (c.g.unib(S.minv < Tol<T>::ZO))                        // :905-908
-        dt = dot(vsub(c.vert(S.av), polytope_centroid(c, S.F, S.F1, S.hw)), dir);
-    if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
+        dt = dot(vsub(c.vert(S.av), polytope_centroid(c, S.F, S.F1, S.hw)), S.dir);
+    if (c.g.unib(dt <= -Tol<T>::ZO)) S.dir = vneg(S.dir);     // :910
     GK_STAMP(SE_DIR);
+    return ST_CONT;
+}
+
+// The rest of an iteration along dir = S.dir: support point(s) (:914, :935-944) and the hull of the polytope
+// vertices and the new point(s) (:918-950).  `first`: iteration 1 after epa_seed, which adds the
+// points to the simplex's tetrahedron exactly as hull_build does (no distance save, no unchanged
+// short cut: iteration 1's termination test compares the seed soup's distances).
+CTX_T DEV int epa_grow(CTX& c, EPAST_T& S, bool first) {
+    constexpr int R = (FC + G - 1) / G;
+    auto& E = c.L.u.e;
+    const int gl = c.g.gl;
+    const V3<T> dir = S.dir;
     const V3<T> sp = support(c, dir);                          // :914
     GK_STAMP(SE_SUP);
     const bool two = c.g.unib(fabs(S.minv) < Tol<T>::ZO);      // :935
-    if (two) {                            // net face count of two insertions unknown: save now
+    if (two && !first) {                  // net face count of two insertions unknown: save now
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int f = r * G + gl;
@@ -903,10 +1008,18 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
         }
     }
     bool ch1 = false, ch2 = false;
-    int st = hull_add(c, S.F, S.kbase, S.hw, S.nv, S.nf, sp, true, 0, ch1, !two);
+    int st = hull_add(c, S.F, S.kbase, S.hw, S.nv, S.nf, sp, true, 0, ch1, !two && !first);
     if (!st && two) st = hull_add(c, S.F, S.kbase, S.hw, S.nv, S.nf, support(c, vneg(dir)), true, 0, ch2, false);
-    S.unchanged = !ch1 && !ch2;
+    S.unchanged = !first && !ch1 && !ch2;
     return st ? st : ST_CONT;
+}
+
+// Closes iteration S.iters; if EPA goes on, runs the next iteration.  ST_CONT, 0 (depth and
+// normal set) or an error status / ST_DEFER.
+CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
+    const int r = epa_close(c, S, depth, normal);
+    if (r != ST_CONT) return r;
+    return epa_grow(c, S, false);
 }
 
 CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf) {
@@ -966,6 +1079,26 @@ CTX_T DEV int hull_band_set(CTX& c, int side, V3<T> n, T mx, T band, bool store)
     return c.g.uni(cnt);
 }
 
+// hull_band_set on precomputed dots: members t > thr (index order) -> LDS sx/sy/sz when `store`
+CTX_T DEV int band_set(CTX& c, int side, const DotSet<T, K>& D, T thr, bool store) {
+    int cnt = 0;
+    auto& C = c.L.u.c;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + c.g.gl;
+        const bool in = i < (side ? c.nb : c.na) && D.t[side][k] > thr;
+        const uint64_t m = c.g.ballot(in);
+        if (store && in) {
+            const V3<T> p = side ? c.BV(k) : c.AV(k);
+            const int pos = cnt + mbcnt(m);
+            C.sx[pos] = p.x; C.sy[pos] = p.y; C.sz[pos] = p.z;
+        }
+        cnt += popc(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return c.g.uni(cnt);
+}
+
 // get_info_collisionType (:353-413)
 CTX_T DEV int collision_type(CTX& c, V3<T> n, T tol) {
     const T m1 = hull_dot_max(c, 0, n);
@@ -975,9 +1108,15 @@ CTX_T DEV int collision_type(CTX& c, V3<T> n, T tol) {
     const int D = hull_band_set(c, 1, nn, m2, tol, false);
     return (C >= 3 && D >= 3) ? 2 : 1;
 }
+// the same from the dots of n already taken (get_nearest_points' pass)
+CTX_T DEV int collision_type(CTX& c, const DotSet<T, K>& D, T tol) {
+    const int na = band_set(c, 0, D, D.m[0] - tol, false);
+    const int nb = band_set(c, 1, D, D.m[1] - tol, false);
+    return (na >= 3 && nb >= 3) ? 2 : 1;
+}
 
 // get_collisionPoint_01 (:700-806)
-CTX_T DEV int contact_v1(CTX& c, V3<T> n, V3<T>& res) {
+CTX_T DEV int contact_v1(CTX& c, V3<T> n, const DotSet<T, K>& D, V3<T>& res) {
     int a0, a1, b0, b1;
     scan_top2(c, 0, n, a0, a1);
     scan_top2(c, 1, vneg(n), b0, b1);
@@ -987,8 +1126,7 @@ CTX_T DEV int contact_v1(CTX& c, V3<T> n, V3<T>& res) {
     if (a0 != a1 && b0 == b1) res = c.B(b0);
     else if (a0 == a1 && b0 != b1) res = c.A(a0);
     if (a0 != a1 && b0 != b1) {
-        const T mx = hull_dot_max(c, 0, n);
-        const int C = hull_band_set(c, 0, n, mx, T(0.1), true);
+        const int C = band_set(c, 0, D, D.m[0] - T(0.1), true);
         T sx = 0, sy = 0, sz = 0;
         for (int i = 0; i < C; ++i) { sx += c.L.u.c.sx[i]; sy += c.L.u.c.sy[i]; sz += c.L.u.c.sz[i]; }
         const T dc = (T)C;
@@ -1146,49 +1284,47 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
 }
 
 // get_collisionPoint_02 (:457-696)
-CTX_T DEV int contact_v2(CTX& c, V3<T> n, V3<T>& res) {
+CTX_T DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
     auto& C = c.L.u.c;
     const T band = T(0.1);
-    const V3<T> nn = vneg(n);
-    const T m1 = hull_dot_max(c, 0, n);
-    const T m2 = hull_dot_max(c, 1, nn);
-    const int n1 = hull_band_set(c, 0, n, m1, band, false);
-    const int n2 = hull_band_set(c, 1, nn, m2, band, false);
+    const T t1 = D.m[0] - band, t2 = D.m[1] - band;                 // :471-472
+    const int n1 = band_set(c, 0, D, t1, false);
+    const int n2 = band_set(c, 1, D, t2, false);
     res = zero3<T>();
     if (n1 == 1 && n2 == 1) {                                      // case_01
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         const V3<T> a = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
         __builtin_amdgcn_wave_barrier();
-        hull_band_set(c, 1, nn, m2, band, true);
+        band_set(c, 1, D, t2, true);
         res = vdiv(vadd(a, vmk<T>(C.sx[0], C.sy[0], C.sz[0])), T(2));
     } else if (n1 == 1 && n2 >= 2) {                               // case_02
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         res = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
     } else if (n1 >= 2 && n2 == 1) {
-        hull_band_set(c, 1, nn, m2, band, true);
+        band_set(c, 1, D, t2, true);
         res = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
     } else if (n1 == 2 && n2 == 2) {                               // case_03
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         const V3<T> a0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), a1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
         __builtin_amdgcn_wave_barrier();
-        hull_band_set(c, 1, nn, m2, band, true);
+        band_set(c, 1, D, t2, true);
         V3<T> f1, f2;
         foot_ll(a0, a1, vmk<T>(C.sx[0], C.sy[0], C.sz[0]), vmk<T>(C.sx[1], C.sy[1], C.sz[1]), f1, f2);
         res = vdiv(vadd(f1, f2), T(2));
     } else if (n1 == 2 && n2 >= 3) {                               // case_04(SPT_p2, SPT_p1)
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
         __builtin_amdgcn_wave_barrier();
-        hull_band_set(c, 1, nn, m2, band, true);
+        band_set(c, 1, D, t2, true);
         return contact_case04(c, n2, q0, q1, res);
     } else if (n1 >= 3 && n2 == 2) {                               // case_04(SPT_p1, SPT_p2)
-        hull_band_set(c, 1, nn, m2, band, true);
+        band_set(c, 1, D, t2, true);
         const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
         __builtin_amdgcn_wave_barrier();
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         return contact_case04(c, n1, q0, q1, res);
     } else if (n1 >= 3 && n2 >= 3) {                               // case_05
-        hull_band_set(c, 0, n, m1, band, true);
+        band_set(c, 0, D, t1, true);
         T sx = 0, sy = 0, sz = 0;
         for (int i = 0; i < n1; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
         const T dn = (T)n1;
@@ -1489,16 +1625,20 @@ CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* 
     int st;
     int ia, ib;
     GK_STAMP(SE_TERM);
-    support_idx(c, n, ia, ib);                                           // get_nearest_points (:326, :813-855)
+    // get_nearest_points (:326, :813-855): one pass of dots along n over both hulls, whose values
+    // and maxima the contact point (v1, v2) and the contact type also use
+    DotSet<T, K> D;
+    support_dots(c, n, D, ia, ib);
     GK_STAMP(SE_NEAR);
     V3<T> pt = zero3<T>();
-    if (version == 1) st = contact_v1(c, n, pt);                          // :329-340
-    else if (version == 2) st = contact_v2(c, n, pt);
-    else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; }
+    bool same_n = true;
+    if (version == 1) st = contact_v1(c, n, D, pt);                       // :329-340
+    else if (version == 2) st = contact_v2(c, D, pt);
+    else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; same_n = false; }
     else st = GJKEPA_STATUS_BAD_VERSION;
     GK_STAMP(SE_CONT);
     if (st) return st;
-    const int type = collision_type(c, n, tol_ff);                        // :343
+    const int type = same_n ? collision_type(c, D, tol_ff) : collision_type(c, n, tol_ff);   // :343
     GK_STAMP(SE_TYPE);
     const V3<T> q1 = c.A(ia), q2 = c.B(ib);
     __builtin_amdgcn_wave_barrier();
@@ -1946,6 +2086,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
     EpaState<T, R> S;
     bool active = false;
+    bool seeded = false;                 // iteration 1 set up by epa_seed: its support step is pending
     int64_t pair = 0;
     uint32_t gjk_it = 0;
     // final record / park / route for a pair whose EPA ended with status r
@@ -1995,9 +2136,15 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
             S.iters = 1; S.nf = 0;
             int r = ST_DEFER;
+            seeded = false;
             if (c.na <= G * K && c.nb <= G * K) {
                 const V3<T> s0 = decode_pt(c, kc[0]), s1 = decode_pt(c, kc[1]), s2 = decode_pt(c, kc[2]), s3 = decode_pt(c, kc[3]);
-                r = epa_begin(c, S, s0, s1, s2, s3);
+#if GJKEPA_EPA_SEED
+                r = epa_seed(c, S, s0, s1, s2, s3);
+                seeded = r == 0;
+                if (r == ST_FALLBACK)
+#endif
+                    r = epa_begin(c, S, s0, s1, s2, s3);
             }
             __builtin_amdgcn_wave_barrier();
             active = r == 0;
@@ -2005,9 +2152,14 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
         }
         GK_STAMP(SE_LOAD);
         if (active) {
+            // groups that closed an iteration (everything but the ones epa_seed just set up) take the
+            // MINLOC / termination step; every continuing group then takes the support step together
             T depth = 0;
             V3<T> n = zero3<T>();
-            const int r = epa_step(c, S, depth, n);
+            int r = ST_CONT;
+            if (!seeded) r = epa_close(c, S, depth, n);
+            if (r == ST_CONT) r = epa_grow(c, S, seeded);
+            seeded = false;
             __builtin_amdgcn_wave_barrier();
             if (r != ST_CONT) {
                 finish(r, depth, n);
