@@ -602,6 +602,186 @@ void run_queries(std::vector<Query*>& qs, int device) {
     }
 }
 
+// ---- resident query service -----------------------------------------------------------------
+// gjkepa_query's fast path: a persistent grid (service_kernel) polls GJKEPA_SVC_SLOTS request slots
+// in host-mapped memory, one wave per slot.  A caller claims a free slot, writes its hull columns and
+// header into it and posts the request's sequence number; the slot's wave answers it with the
+// one-wave query path and posts the record back into the slot, which the caller polls.  No launch,
+// copy or stream synchronisation per call: one bus read of the request line, one of the hulls and
+// the record's write back.  The grid drains by itself after GJKEPA_SVC_IDLE_US without a request
+// (or at process exit); the next caller relaunches it.  More concurrent callers than slots, and
+// GJKEPA_QUERY_SERVICE=0, take the combining path above.
+#ifndef GJKEPA_SVC_IDLE_US
+#define GJKEPA_SVC_IDLE_US 2000
+#endif
+struct Service {
+    std::mutex mu;                            // launches
+    int device = 0, ok = 0;                   // ok: 1 ready, -1 unavailable
+    gjkepa_svc_slot* slots = nullptr;         // host view
+    gjkepa_svc_slot* dslots = nullptr;        // device view
+    gjkepa_svc_ctrl* ctrl = nullptr;          // device memory
+    uint32_t* closing = nullptr;              // host-mapped word the draining grid writes its generation to
+    uint32_t* dclosing = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;                  // recorded after each grid
+    std::atomic<uint32_t> gen{0};             // generation of the latest grid (0: none launched)
+    std::atomic<uint64_t> free_slots{GJKEPA_SVC_SLOTS >= 64 ? ~0ull : (1ull << GJKEPA_SVC_SLOTS) - 1ull};
+    uint32_t seq[GJKEPA_SVC_SLOTS] = {};      // last posted sequence number, owned by the slot's holder
+    uint64_t idle_ticks = 0;
+};
+static_assert(GJKEPA_SVC_SLOTS >= 1 && GJKEPA_SVC_SLOTS <= 64, "service slot bitmap");
+std::mutex g_svc_mu;
+std::vector<Service*> g_svc;
+bool g_svc_exit_hook = false;
+
+void service_shutdown() {                     // atexit: every wave sees its stop word and leaves
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    for (Service* sv : g_svc) {
+        if (!sv || sv->ok != 1 || sv->gen.load() == 0) continue;
+        for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 1u, __ATOMIC_RELEASE);
+        (void)hipEventSynchronize(sv->ev);
+    }
+}
+
+bool service_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("GJKEPA_QUERY_SERVICE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// the device's service, set up on first use (nullptr: unavailable, the caller combines instead)
+Service* service(int device) {
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    if ((int)g_svc.size() <= device) g_svc.resize((size_t)device + 1, nullptr);
+    Service*& sv = g_svc[(size_t)device];
+    if (sv) return sv->ok == 1 ? sv : nullptr;
+    sv = new Service();
+    sv->device = device;
+    sv->ok = -1;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    void* h = nullptr;
+    void* hc = nullptr;
+    int rate_khz = 0;
+    if (hipHostMalloc(&h, sizeof(gjkepa_svc_slot) * GJKEPA_SVC_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return nullptr;
+    sv->slots = (gjkepa_svc_slot*)h;
+    std::memset(h, 0, sizeof(gjkepa_svc_slot) * GJKEPA_SVC_SLOTS);
+    if (hipHostMalloc(&hc, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    sv->closing = (uint32_t*)hc;
+    std::memset(hc, 0, 64);
+    void* dv = nullptr;
+    if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess) return nullptr;
+    sv->dslots = (gjkepa_svc_slot*)dv;
+    if (hipHostGetDevicePointer(&dv, hc, 0) != hipSuccess) return nullptr;
+    sv->dclosing = (uint32_t*)dv;
+    if (hipMalloc(&dv, sizeof(gjkepa_svc_ctrl)) != hipSuccess || hipMemset(dv, 0, sizeof(gjkepa_svc_ctrl)) != hipSuccess)
+        return nullptr;
+    sv->ctrl = (gjkepa_svc_ctrl*)dv;
+    if (hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sv->ev, hipEventDisableTiming) != hipSuccess ||
+        hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || rate_khz <= 0)
+        return nullptr;
+    sv->idle_ticks = (uint64_t)rate_khz * GJKEPA_SVC_IDLE_US / 1000;
+    if (!g_svc_exit_hook) {
+        std::atexit(service_shutdown);        // registered after the runtime's own: runs before its teardown
+        g_svc_exit_hook = true;
+    }
+    sv->ok = 1;
+    return sv;
+}
+
+// make sure a grid newer than `seen` (or any grid, seen == 0) is serving: relaunch when none was
+// launched, the latest one is draining (it wrote its generation to `closing`), or `check_done` and
+// the latest one has finished
+int service_ensure(Service* sv, bool check_done) {
+    const uint32_t g0 = sv->gen.load(std::memory_order_acquire);
+    if (g0 != 0 && __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) != g0 && !check_done) return 0;
+    std::lock_guard<std::mutex> g(sv->mu);
+    const uint32_t g1 = sv->gen.load(std::memory_order_relaxed);
+    if (g1 != g0) return 0;                   // another caller relaunched meanwhile
+    hipError_t e;
+    if (g1 != 0) {
+        bool need = __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) == g1;
+        if (!need && check_done) {
+            e = hipEventQuery(sv->ev);
+            if (e != hipSuccess && e != hipErrorNotReady) return hip_fail(e, "query service");
+            need = e == hipSuccess;
+        }
+        if (!need) return 0;
+        if ((e = hipEventSynchronize(sv->ev)) != hipSuccess) return hip_fail(e, "query service drain");
+    }
+    if ((e = hipSetDevice(sv->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    uint32_t ng = g1 + 1;
+    if (ng == 0) ng = 1;
+    gjkepa_svc_args a{sv->dslots, sv->ctrl, sv->dclosing, ng, sv->idle_ticks};
+    if ((e = gjkepa_launch_service(a, GJKEPA_SVC_SLOTS, sv->stream)) != hipSuccess) return hip_fail(e, "query service launch");
+    if ((e = hipEventRecord(sv->ev, sv->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    sv->gen.store(ng, std::memory_order_release);
+    return 0;
+}
+
+// GJKEPA_QUERY_STATS=1: calls served, mean round trip and mean device time per call, printed at exit
+struct ServiceStats {
+    std::atomic<int64_t> calls{0}, ns{0}, dev_ticks{0}, tick_khz{0};
+    bool on = std::getenv("GJKEPA_QUERY_STATS") != nullptr;
+    ~ServiceStats() {
+        if (on && calls > 0 && tick_khz > 0)
+            std::fprintf(stderr, "gjkepa_query service: %lld calls, %.2f us/call round trip, %.2f us/call on the device\n",
+                         (long long)calls.load(), 1e-3 * (double)ns / (double)calls,
+                         1e3 * (double)dev_ticks / (double)tick_khz / (double)calls);
+    }
+} g_sstats;
+
+int service_claim(Service* sv) {
+    uint64_t f = sv->free_slots.load(std::memory_order_relaxed);
+    while (f) {
+        const int k = __builtin_ctzll(f);
+        if (sv->free_slots.compare_exchange_weak(f, f & ~(1ull << k), std::memory_order_acquire)) return k;
+    }
+    return -1;
+}
+
+// one pair through slot k; the record lands in *rec
+int service_run(Service* sv, int k, int32_t version, double tol_ff, const double* p1, int32_t n1, const double* p2,
+                int32_t n2, gjkepa_contact_f64* rec) {
+    gjkepa_svc_slot* sl = &sv->slots[k];
+    std::memcpy(sl->v, p1, sizeof(double) * 3 * (size_t)n1);
+    std::memcpy(sl->v + 3 * (size_t)n1, p2, sizeof(double) * 3 * (size_t)n2);
+    sl->version = version;
+    sl->na = n1;
+    sl->nb = n2;
+    sl->tol_ff = tol_ff;
+    uint32_t seq = sv->seq[k] + 1;
+    if (seq == 0) seq = 1;
+    sv->seq[k] = seq;
+    __atomic_store_n(&sl->req, seq, __ATOMIC_RELEASE);
+    int rc = service_ensure(sv, false);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto next_check = t0 + std::chrono::microseconds(200);
+    for (uint32_t spin = 1; __atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+        __builtin_ia32_pause();
+        if ((spin & 63u) == 0) {
+            const auto now = std::chrono::steady_clock::now();
+            if (now >= next_check) {              // the grid may have drained under this request
+                if ((rc = service_ensure(sv, true)) != 0) return rc;
+                next_check = now + std::chrono::microseconds(200);
+                if (now - t0 > std::chrono::seconds(30)) return fail(GJKEPA_E_HIP, "query service: no answer in 30 s");
+            }
+        }
+    }
+    std::memcpy(rec, sl->rec, sizeof(gjkepa_contact_f64));
+    if (g_sstats.on) {
+        g_sstats.calls += 1;
+        g_sstats.ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        g_sstats.dev_ticks += (int64_t)(sl->t_done - sl->t_seen);
+        g_sstats.tick_khz = (int64_t)(sv->idle_ticks * 1000 / GJKEPA_SVC_IDLE_US);
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -615,8 +795,15 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
     int rc = 0;
     if (!device_state(device, &rc)) return rc;
-    Combiner* cb = combiner(device);
     Query me{version, tol_ff, p1, p2, n1, n2, {}};
+    Service* sv = service_enabled() && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS ? service(device) : nullptr;
+    const int slot = sv ? service_claim(sv) : -1;
+    if (slot >= 0) {
+        rc = service_run(sv, slot, version, tol_ff, p1, n1, p2, n2, &me.rec);
+        sv->free_slots.fetch_or(1ull << slot, std::memory_order_release);
+        if (rc) return rc;
+    } else {
+    Combiner* cb = combiner(device);
     {
         std::unique_lock<std::mutex> lk(cb->mu);
         cb->queue.push_back(&me);
@@ -655,6 +842,7 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
         rc = me.rc;
     }
     if (rc) return fail(rc, me.err);
+    }
     const gjkepa_contact_f64& r = me.rec;
     *collision = r.collision;
     *colli_type = r.colli_type;

@@ -119,6 +119,13 @@
 #ifndef GJKEPA_E4_MINW
 #define GJKEPA_E4_MINW 1
 #endif
+// one-wave query path (query_kernel, the resident query service): EPA's first polytope
+#ifndef GJKEPA_Q_VCAP
+#define GJKEPA_Q_VCAP 40
+#endif
+#ifndef GJKEPA_Q_FCAP
+#define GJKEPA_Q_FCAP 64
+#endif
 // contact-feature tiers (nearest points, contact point, contact type): G, K as above
 #ifndef GJKEPA_C0_G
 #define GJKEPA_C0_G 8
@@ -293,3 +300,34 @@ hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const 
 hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
 // the chain's counter / tally reset (n32 uint32 words from ws); a kernel node rather than a memset node
 hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s);
+
+// ---- resident query service (gjkepa_query): a grid of one-wave workgroups, wave w serving request
+// slot w, that polls host-mapped request slots and answers each posted pair with query_pair.  A
+// slot's request line is written by the host (payload and header first, `req` last, release), its
+// completion line by the device (record first, `done` last, release); each side polls the other's.
+#ifndef GJKEPA_SVC_SLOTS
+#define GJKEPA_SVC_SLOTS 64
+#endif
+struct alignas(128) gjkepa_svc_slot {
+    uint32_t req, stop;              // posted request's sequence number; nonzero: the serving wave exits
+    int32_t version, na, nb, pad0;
+    double tol_ff;
+    uint32_t pad1[24];
+    uint32_t done, pad2;             // sequence number of the last answered request
+    uint64_t t_seen, t_done;         // device wall clock when it was seen / answered (GJKEPA_QUERY_STATS)
+    uint32_t pad3[26];
+    uint64_t rec[16];                // its gjkepa_contact_f64 record
+    double v[3 * 2 * GJKEPA_MAX_HULL_VERTS];   // hull A columns (x, y, z), then hull B's
+};
+struct gjkepa_svc_ctrl {             // device memory, one per service
+    uint32_t closing, pad;           // generation whose grid is draining
+    uint64_t last;                   // wall clock of the latest answered request
+};
+struct gjkepa_svc_args {
+    gjkepa_svc_slot* slots;          // device view of the host-mapped slots
+    gjkepa_svc_ctrl* ctrl;
+    uint32_t* host_closing;          // device view of a host-mapped word: generation that is draining
+    uint32_t gen;                    // this grid's generation (nonzero)
+    uint64_t idle_ticks;             // wall-clock ticks without a request anywhere before the grid drains
+};
+hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStream_t s);

@@ -2172,37 +2172,31 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     tally_end(a.tally);
 }
 
-// One-kernel query path for small batches (combined single-pair queries, gjkepa_query): one wave per
-// pair runs the sphere test, GJK, EPA and the contact features back to back with the largest tier's
-// capacities (64 lanes, hulls up to 256 vertices, EPA tier 4's polytope: never defers), so a batch
-// costs one launch instead of the tier chain's ten.  Same device functions as the tier kernels, so
-// the records are the chain's bit for bit.
-template <typename TIn, typename T>
-__global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
-    constexpr int G = 64, K = GJKEPA_MAX_HULL_VERTS / 64, VC = GJKEPA_E4_VCAP, FC = GJKEPA_E4_FCAP;
-    using L_t = Lds<T, TIn, G, K, VC, FC, true>;
-    extern __shared__ __align__(16) unsigned char smem[];
-    L_t& L = *reinterpret_cast<L_t*>(smem);
-    const Grp<G> grp;
+// One-wave query path (small batches, gjkepa_query's combined batches and its resident service):
+// one wave per pair runs the sphere test, GJK, EPA and the contact features back to back, so a pair
+// costs no tier chain.  Tuned for the latency of one pair on an otherwise idle wave: the hull
+// register depth K (64K vertices per hull) is picked per pair from its larger hull, and EPA first
+// runs with a small polytope (GJKEPA_Q_VCAP / GJKEPA_Q_FCAP: one face row per lane) and only on
+// overflow restarts from the GJK simplex with EPA tier 4's polytope, as the tier chain's deferral
+// does.  Same device functions as the tier kernels, so the records are the chain's bit for bit.
+template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, true>;
+template <typename TIn, typename T, int K> using QLdsS = Lds<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, true>;
+template <typename TIn, typename T, int K>
+DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
+                      int version, T tol_ff, void* out, int64_t pair) {
+    using LB = QLds<TIn, T, K>;
+    using LS = QLdsS<TIn, T, K>;
+    static_assert(__builtin_offsetof(LB, u) == __builtin_offsetof(LS, u) && sizeof(LS) <= sizeof(LB),
+                  "the two polytopes share the hull image");
     const int gl = grp.gl;
-    const int64_t pair = blockIdx.x;
-    GK_GUARD(5, 0);
-    if (pair >= a.n_pairs) return;
-    const TIn* verts = (const TIn*)a.verts;
-    Ctx<T, TIn, G, K, VC, FC, 2> c{L, grp};
-    const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
-    const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
+    Ctx<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, 2> c{*reinterpret_cast<QLdsS<TIn, T, K>*>(smem), grp};
     T o13[13];
 #pragma unroll
     for (int i = 0; i < 13; ++i) o13[i] = T(0);
-    if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
-        store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
-        return;
-    }
     c.na = na;
     c.nb = nb;
-    if (load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb])) {
-        store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+    if (load_hulls(c, pa, pb)) {
+        store_record<64, T>(out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
         return;
     }
     uint32_t kc[4];
@@ -2210,11 +2204,11 @@ __global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
     int r = gjk_phase(c, kc, gjk_it, GJKEPA_AXIS_REJECT != 0);
     __builtin_amdgcn_wave_barrier();
     if (r == PH_MISS) {
-        store_record<G, T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
+        store_record<64, T>(out, pair, gl, o13, 0, 0, 0, 0u);
         return;
     }
     if (r != PH_HIT) {                                   // GJK-phase error (reference would STOP)
-        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
+        store_record<64, T>(out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
         return;
     }
     T depth;
@@ -2222,19 +2216,128 @@ __global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
     uint32_t de = 0;
     r = epa_phase(c, kc, depth, n, de);
     __builtin_amdgcn_wave_barrier();
+    if (r == ST_DEFER) {                                 // small polytope full: tier 4's from the simplex
+        Ctx<T, TIn, 64, K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, 2> cb{*reinterpret_cast<QLds<TIn, T, K>*>(smem), grp};
+        cb.na = na;
+        cb.nb = nb;
+        cb.vmax_a = c.vmax_a;
+        cb.vmax_b = c.vmax_b;
+        r = epa_phase(cb, kc, depth, n, de);
+        __builtin_amdgcn_wave_barrier();
+    }
     const uint32_t diag = ((uint32_t)gjk_it & 0xffu) | de;
     if (r != 0) {                                        // last tier out of capacity: DEGENERATE
-        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
+        store_record<64, T>(out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
         return;
     }
-    r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
+    r = contact_phase(c, depth, n, version, tol_ff, o13);
     __builtin_amdgcn_wave_barrier();
     if (r < 0) {
-        store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
+        store_record<64, T>(out, pair, gl, o13, 1, -r, 0, diag);
     } else {
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
-        store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, diag);
+        store_record<64, T>(out, pair, gl, o13, 1, 0, r, diag);
+    }
+}
+
+// one pair on this wave: hull depth from the larger hull; bad sizes answered BAD_INPUT
+template <typename TIn, typename T>
+DEV void query_pair(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
+                    int version, T tol_ff, void* out, int64_t pair) {
+    const int nmax = na > nb ? na : nb;
+    if (na < 1 || nb < 1 || nmax > GJKEPA_MAX_HULL_VERTS) {
+        T o13[13];
+#pragma unroll
+        for (int i = 0; i < 13; ++i) o13[i] = T(0);
+        store_record<64, T>(out, pair, grp.gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+    } else if (nmax <= 64) {
+        query_pair_k<TIn, T, 1>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+    } else if (nmax <= 128) {
+        query_pair_k<TIn, T, 2>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+    } else {
+        query_pair_k<TIn, T, GJKEPA_MAX_HULL_VERTS / 64>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+    }
+}
+
+template <typename TIn, typename T>
+__global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<64> grp;
+    const int64_t pair = blockIdx.x;
+    GK_GUARD(5, 0);
+    if (pair >= a.n_pairs) return;
+    const TIn* verts = (const TIn*)a.verts;
+    const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+    const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
+    query_pair<TIn, T>(smem, grp, verts + a.hull_off[ha], verts + a.hull_off[hb], na, nb, a.version, (T)a.tol_ff,
+                       a.out, pair);
+}
+
+// Resident query service (gjkepa_query, include/gjkepa.h): wave w serves request slot w of
+// host-mapped memory.  It polls the slot's request line (one lane, system-scope acquire), answers a
+// new request with query_pair straight from the slot (hull columns read once over the bus into
+// LDS; the record stored into the slot) and publishes it with a system-scope release of `done`.
+// Every wave leaves once the host sets its slot's stop word, or once no slot has been answered for
+// idle_ticks (the first wave to see that marks the generation closing for the others and for the
+// host, which relaunches the grid for the next request), so the grid always drains by itself.
+DEV uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+__global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<64> grp;
+    gjkepa_svc_slot* sl = a.slots + blockIdx.x;
+    const uint32_t* hdr = &sl->req;
+    uint32_t last = uni32(__hip_atomic_load(&sl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    uint64_t seen = wall_clock64();
+    int empty = 0;
+    for (;;) {
+        // request line words 0, 1 (req, stop): relaxed system-scope reads (no cache invalidation
+        // per poll); the acquire fence is paid once per new request
+        uint32_t w = 0;
+        if (grp.lane < 2) w = __hip_atomic_load(hdr + grp.lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t req = uni32(w);
+        const uint32_t stop = (uint32_t)__builtin_amdgcn_readlane((int)w, 1);
+        if (req != last) {
+            const uint64_t t_seen = wall_clock64();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // header and hulls are read after req
+            GK_STAMP_BEGIN();
+            uint32_t h = 0;
+            if (grp.lane < 8) h = __hip_atomic_load(hdr + grp.lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const int version = __builtin_amdgcn_readlane((int)h, 2);
+            const int na = __builtin_amdgcn_readlane((int)h, 3), nb = __builtin_amdgcn_readlane((int)h, 4);
+            const uint64_t tb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h, 6) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h, 7) << 32);
+            const double tol = __builtin_bit_cast(double, tb);
+            const int ca = na < 0 || na > GJKEPA_MAX_HULL_VERTS ? 0 : na;
+            query_pair<double, double>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
+            __builtin_amdgcn_wave_barrier();
+            GK_STAMP_END();
+            const uint64_t t_done = wall_clock64();
+            if (grp.lane == 0) {
+                sl->t_seen = t_seen;
+                sl->t_done = t_done;
+                __hip_atomic_store(&sl->done, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_max(&a.ctrl->last, t_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            last = req;
+            seen = wall_clock64();
+            empty = 0;
+            continue;
+        }
+        if (stop) break;
+        if (uni32(__hip_atomic_load(&a.ctrl->closing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.gen) break;
+        const uint64_t now = wall_clock64();
+        const uint64_t g = __hip_atomic_load(&a.ctrl->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t act = g > seen ? g : seen;
+        if (now > act && now - act > a.idle_ticks) {
+            if (grp.lane == 0) {
+                __hip_atomic_store(&a.ctrl->closing, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.host_closing, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            break;
+        }
+        if (++empty > 64) __builtin_amdgcn_s_sleep(32);    // quiet slot: a poll about every microsecond
     }
 }
 
@@ -2416,8 +2519,14 @@ extern "C" int gjkepa_diag_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStream_t s) {
+    using L_t = gk::QLds<double, double, GJKEPA_MAX_HULL_VERTS / 64>;
+    hipLaunchKernelGGL(gk::service_kernel, dim3((unsigned)n_slots), dim3(64), sizeof(L_t), s, a);
+    return hipGetLastError();
+}
+
 template <typename TIn, typename T> hipError_t launch_query(const gjkepa_epa_args& a, hipStream_t s) {
-    using L_t = gk::Lds<T, TIn, 64, GJKEPA_MAX_HULL_VERTS / 64, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, true>;
+    using L_t = gk::QLds<TIn, T, GJKEPA_MAX_HULL_VERTS / 64>;
     auto kfn = gk::query_kernel<TIn, T>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)a.n_pairs), dim3(64), sizeof(L_t), s, a);
     return hipGetLastError();
