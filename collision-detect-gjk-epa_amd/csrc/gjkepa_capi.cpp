@@ -651,8 +651,26 @@ bool service_enabled() {
     return on;
 }
 
+// lock-free view of the services that are ready (per call: no mutex, no runtime query)
+constexpr int kSvcDevMax = 64;
+std::atomic<Service*> g_svc_ready[kSvcDevMax];
+std::atomic<int> g_ndev{-1};
+
+int device_count_cached() {
+    int n = g_ndev.load(std::memory_order_relaxed);
+    if (n < 0) {
+        if (hipGetDeviceCount(&n) != hipSuccess || n < 0) n = 0;
+        g_ndev.store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
 // the device's service, set up on first use (nullptr: unavailable, the caller combines instead)
 Service* service(int device) {
+    if (device >= 0 && device < kSvcDevMax) {
+        Service* r = g_svc_ready[device].load(std::memory_order_acquire);
+        if (r) return r;
+    }
     std::lock_guard<std::mutex> g(g_svc_mu);
     if ((int)g_svc.size() <= device) g_svc.resize((size_t)device + 1, nullptr);
     Service*& sv = g_svc[(size_t)device];
@@ -689,6 +707,7 @@ Service* service(int device) {
         g_svc_exit_hook = true;
     }
     sv->ok = 1;
+    if (device < kSvcDevMax) g_svc_ready[device].store(sv, std::memory_order_release);
     return sv;
 }
 
@@ -794,10 +813,11 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
         return fail(GJKEPA_E_ARG, "null pointer");
     if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
     int rc = 0;
-    if (!device_state(device, &rc)) return rc;
     Query me{version, tol_ff, p1, p2, n1, n2, {}};
-    Service* sv = service_enabled() && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS ? service(device) : nullptr;
+    Service* sv = service_enabled() && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS &&
+                  device >= 0 && device < device_count_cached() ? service(device) : nullptr;
     const int slot = sv ? service_claim(sv) : -1;
+    if (slot < 0 && !device_state(device, &rc)) return rc;
     if (slot >= 0) {
         rc = service_run(sv, slot, version, tol_ff, p1, n1, p2, n2, &me.rec);
         sv->free_slots.fetch_or(1ull << slot, std::memory_order_release);

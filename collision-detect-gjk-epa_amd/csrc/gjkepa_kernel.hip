@@ -98,7 +98,7 @@ DEV void guard_report(uint32_t kid, uint32_t want, uint32_t got) {
 
 enum { SG_LOAD = 0, SG_SPHERE, SG_INIT, SG_UPD, SG_CHK, SG_STORE, SG_ROUTE,
        SE_LOAD = 10, SE_IT1, SE_DIR, SE_SUP, SE_VIS, SE_HOR, SE_CMP, SE_CONE, SE_TERM, SE_NEAR, SE_CONT, SE_TYPE,
-       SE_STORE, SE_ROUTE };
+       SE_STORE, SE_ROUTE, SC_ROUTE, SC_LOAD, SC_STORE };
 
 
 // ---------------------------------------------------------------- per-group LDS image
@@ -2337,7 +2337,10 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
             }
             break;
         }
-        if (++empty > 64) __builtin_amdgcn_s_sleep(32);    // quiet slot: a poll about every microsecond
+        // a slot that just answered polls back to back; a quiet one about every microsecond, a
+        // long-quiet one (callers take the lowest free slot) about every 8 microseconds
+        if (++empty > 64) __builtin_amdgcn_s_sleep(32);
+        if (empty > 4096) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }
     }
 }
 
@@ -2357,7 +2360,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
     for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, a.grid == GJKEPA_GRID_UNITS, [&](int64_t pair) {
-        GK_STAMP(SE_ROUTE);
+        GK_STAMP(SC_ROUTE);
         Ctx<T, TIn, G, K, 0, 1, LH> c{L, grp};
         const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
         c.na = grp.uni(a.hull_cnt[ha]);
@@ -2367,7 +2370,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
         const V3<T> n = vmk<T>(rec[1], rec[2], rec[3]);
         const uint32_t diag = reinterpret_cast<const uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + (sizeof(T) == 8 ? 27 : 14)];
         load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
-        GK_STAMP(SE_LOAD);
+        GK_STAMP(SC_LOAD);
         T o13[13];
 #ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
         const int r = -1;
@@ -2386,9 +2389,9 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
         }
         if (gl == 0) a.route[pair] = 0;
         __builtin_amdgcn_wave_barrier();
-        GK_STAMP(SE_STORE);
+        GK_STAMP(SC_STORE);
     });
-    GK_STAMP(SE_ROUTE);
+    GK_STAMP(SC_ROUTE);
     tally_end(a.tally);
     GK_STAMP_END();
 }

@@ -51,6 +51,11 @@ PROGRAM bench_callpattern
 
     CALL GJKEPA_BATCH(2, 1.D0, verts, hoff, hcnt, prs(:, 1:1), bh(1:1), btyp(1:1), bnp(:,:,1:1), bn(:,1:1), &
                       bp(:,1:1), bd(1:1), bst(1:1))                        ! device warm-up
+    DO j = 1, 3                                                                ! query path set-up
+        A(:, j) = verts(hoff(1) + (j-1)*NV : hoff(1) + j*NV - 1)
+        B(:, j) = verts(hoff(2) + (j-1)*NV : hoff(2) + j*NV - 1)
+    END DO
+    CALL GJKEPA(2, 1.D0, A, B, hit, typ, npt, nrm, cpt, dep)
     t0 = OMP_GET_WTIME()
     !$OMP PARALLEL DO PRIVATE(A, B, hit, typ, npt, nrm, cpt, dep, j) SCHEDULE(DYNAMIC, 16)
     DO i = 1, n

@@ -18,7 +18,8 @@ from bench import CONFIGS, SEED  # noqa: E402
 NAMES = {0: "gjk.load", 1: "gjk.sphere", 2: "gjk.init", 3: "gjk.update_simplex", 4: "gjk.checks+inside",
          5: "gjk.store", 6: "gjk.route", 10: "epa.load", 11: "epa.iter1", 12: "epa.dir", 13: "epa.support",
          14: "epa.visible", 15: "epa.horizon", 16: "epa.compact", 17: "epa.cone", 18: "epa.term",
-         19: "epa.nearest", 20: "epa.contact", 21: "epa.type", 22: "epa.store", 23: "epa.route"}
+         19: "ct.nearest", 20: "ct.contact", 21: "ct.type", 22: "epa.store", 23: "epa.route",
+         24: "ct.route", 25: "ct.load", 26: "ct.store"}
 
 
 def main():
@@ -33,7 +34,7 @@ def main():
     lib.gjkepa_diag_stamps(buf.ctypes.data, 1)
     gjkepa.gjkepa_batch(pool, 2, 1.0, gjkepa.PREC_F64)
     lib.gjkepa_diag_stamps(buf.ctypes.data, 1)
-    for lo, hi, title in ((0, 10, "GJK kernels"), (10, 32, "EPA kernels")):
+    for lo, hi, title in ((0, 10, "GJK kernels"), (10, 32, "EPA + contact kernels")):
         tot = float(buf[lo:hi].sum())
         print(f"== {cfg} {title}: {tot / n:.0f} wave-ticks per pair")
         for i in range(lo, hi):
