@@ -132,8 +132,9 @@ int num_cus_current() {
 // pass, was 2.5% slower on C2.)
 // Each fork point gets its own internal stream (GJKEPA_FORK_STREAMS 2; 1: one shared stream, the
 // passes in order), so a small pass forked late does not queue behind the big pass of tier 0.  The
-// internal streams run at the lowest stream priority (GJKEPA_FORK_LOWPRIO): the EPA tiers on the
-// caller's stream are dispatched first as the pass's workgroups free wave slots.  The last fork
+// internal streams run at the highest stream priority (GJKEPA_FORK_PRIO 1; 0 default, -1 lowest):
+// the forked pass of EPA tier 0 is the C2 chain's critical path, while the EPA tiers beside it serve
+// a few long pairs (A/B r3: C2 144.5 vs 143.9 M/s at the lowest priority; C4 / C5 unchanged).  The last fork
 // point's pass runs on the caller's stream (GJKEPA_LAST_PASS_MAIN): nothing follows it to overlap.
 #ifndef GJKEPA_FORK_MASK
 #define GJKEPA_FORK_MASK 0x15
@@ -141,8 +142,8 @@ int num_cus_current() {
 #ifndef GJKEPA_FORK_STREAMS
 #define GJKEPA_FORK_STREAMS 2
 #endif
-#ifndef GJKEPA_FORK_LOWPRIO
-#define GJKEPA_FORK_LOWPRIO 1
+#ifndef GJKEPA_FORK_PRIO
+#define GJKEPA_FORK_PRIO 1
 #endif
 #ifndef GJKEPA_LAST_PASS_MAIN
 #define GJKEPA_LAST_PASS_MAIN 1
@@ -171,12 +172,13 @@ int fork_state(hipStream_t s, Fork** out) {
         if (kv.first.dev == dev && kv.first.caller == s) { *out = kv.second; return 0; }
     if (g_fork.size() >= kForkMax) return 0;
     Fork* f = new Fork();
-    int least = 0, greatest = 0;
-    if (!GJKEPA_FORK_LOWPRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    int least = 0, greatest = 0, prio = 0;
+    if (GJKEPA_FORK_PRIO != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        prio = GJKEPA_FORK_PRIO > 0 ? greatest : least;
     for (int t = 0; t < GJKEPA_EPA_TIERS && e == hipSuccess; ++t) {
         // a stream per fork point that forks (the first one only when shared)
         const bool forks = ((GJKEPA_FORK_MASK >> t) & 1) && !(GJKEPA_LAST_PASS_MAIN && t == GJKEPA_EPA_TIERS - 1);
-        if (forks && (GJKEPA_FORK_STREAMS > 1 || !f->s2[0])) e = hipStreamCreateWithPriority(&f->s2[t], hipStreamNonBlocking, least);
+        if (forks && (GJKEPA_FORK_STREAMS > 1 || !f->s2[0])) e = hipStreamCreateWithPriority(&f->s2[t], hipStreamNonBlocking, prio);
         else if (forks) f->s2[t] = f->s2[0];
         if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[t], hipEventDisableTiming);
@@ -625,7 +627,7 @@ struct Service {
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;                  // recorded after each grid
     std::atomic<uint32_t> gen{0};             // generation of the latest grid (0: none launched)
-    std::atomic<uint64_t> free_slots{GJKEPA_SVC_SLOTS >= 64 ? ~0ull : (1ull << GJKEPA_SVC_SLOTS) - 1ull};
+    std::atomic<uint64_t> free_slots{~0ull >> (64 - GJKEPA_SVC_SLOTS)};
     uint32_t seq[GJKEPA_SVC_SLOTS] = {};      // last posted sequence number, owned by the slot's holder
     uint64_t idle_ticks = 0;
 };
