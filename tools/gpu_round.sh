@@ -4,7 +4,7 @@
 # call-pattern benchmark (OpenMP loop of single GJKEPA calls vs one GJKEPA_BATCH).
 # Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [skip-tests]
 set -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -17,7 +17,7 @@ fi
 echo "== bench C2 $(date)" && timeout -k 10 400 python bench.py > $OUT/bench_c2.json 2> $OUT/bench_c2.err && cat $OUT/bench_c2.json && \
 echo "== rocprof C2 $(date)" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-f32-leg --no-warm-leg > $OUT/prof_bench.json 2> $OUT/prof.err && \
 echo "== pmc $(date)" && timeout -k 10 600 bash tools/pmc.sh $TAG > $OUT/pmc.log 2>&1 && cat $OUT/pmc.log && \
-echo "== call pattern $(date)" && OMP_NUM_THREADS=16 timeout -k 10 300 tests/fortran/build/bench_callpattern 100000 > $OUT/callpattern.txt 2>&1 && cat $OUT/callpattern.txt && \
+echo "== call pattern $(date)" && bash tools/callpattern_probe.sh $TAG/callpattern 5000 100000 && \
 echo "== done $(date)" || exit 1
 if [ -n "$CFGS45" ]; then
   for c in C4 C5; do

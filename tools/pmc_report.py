@@ -29,14 +29,14 @@ def main():
     for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            if "gk::" not in k or k.endswith(", true>"):   # the bench's warm-start leg is not the chain
+            if "gk::" not in k or (k.startswith("gk::gjk_kernel") and k.endswith(", true>")):   # warm-start GJK: not the chain
                 continue
             d = per[k][r["Counter_Name"]]
             d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     for f in sorted(glob.glob(f"{base}/p*/run_kernel_trace.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            if "gk::" not in k or k.endswith(", true>"):   # the bench's warm-start leg is not the chain
+            if "gk::" not in k or (k.startswith("gk::gjk_kernel") and k.endswith(", true>")):   # warm-start GJK: not the chain
                 continue
             dur[k][f + r.get("Dispatch_Id", "")] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     # one chain = one dispatch of GJK tier 0 (it takes every pair); a kernel dispatched several times
