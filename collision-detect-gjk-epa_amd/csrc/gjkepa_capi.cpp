@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gjkepa.h"
@@ -137,7 +138,7 @@ int num_cus_current() {
 // a few long pairs (A/B r3: C2 144.5 vs 143.9 M/s at the lowest priority; C4 / C5 unchanged).  The last fork
 // point's pass runs on the caller's stream (GJKEPA_LAST_PASS_MAIN): nothing follows it to overlap.
 #ifndef GJKEPA_FORK_MASK
-#define GJKEPA_FORK_MASK 0x15
+#define GJKEPA_FORK_MASK 0x25
 #endif
 #ifndef GJKEPA_FORK_STREAMS
 #define GJKEPA_FORK_STREAMS 2
@@ -195,13 +196,13 @@ int fork_state(hipStream_t s, Fork** out) {
 // hull capacity (vertices) of EPA tier t (gjkepa_kernel.hip: epa_hull_cap)
 constexpr int epa_hull_cap(int t) {
     return t == 0 ? GJKEPA_E0_G * GJKEPA_E0_K : t == 1 ? GJKEPA_E1_G * GJKEPA_E1_K : t == 2 ? GJKEPA_E2_G * GJKEPA_E2_K
-         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : GJKEPA_E4_G * GJKEPA_E4_K;
+         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : t == 4 ? GJKEPA_E4_G * GJKEPA_E4_K : GJKEPA_E5_G * GJKEPA_E5_K;
 }
 
 // Fork points of an overlapped chain (bit t: a contact pass is forked after EPA tier t).  The pairs
 // EPA tier t finishes go to the contact pass of the first fork point p >= t (route code
 // GJKEPA_ROUTE_CT(p) + contact tier).  Default: after tier 0 (C2's hits), after tier 2 (C4 / C5's
-// 33-128-vertex hulls, with tier 1's few overflow pairs) and after the last tier (tiers 3-4): three
+// 33-128-vertex hulls, with tier 1's few overflow pairs) and after the last tier (tiers 3-5): three
 // forks and five contact launches instead of one fork and up to two launches per tier, so the short
 // tail of a C2 chain carries three fewer near-empty launches.
 static_assert((GJKEPA_FORK_MASK >> (GJKEPA_EPA_TIERS - 1)) & 1, "the last EPA tier is a fork point");
@@ -407,16 +408,18 @@ const char* gjkepa_version_string(void) {
     static char buf[800];
     std::snprintf(buf, sizeof(buf),
                   "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
-                  "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
-                  "waves/SIMD G%d%d E%d%d%d%d%d C%d%d; LDS-hull G%d%d E%d%d%d%d%d C%d%d; "
+                  "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
+                  "waves/SIMD G%d%d E%d%d%d%d%d%d C%d%d; LDS-hull G%d%d E%d%d%d%d%d%d C%d%d; "
                   "-O3 -ffp-contract=off; src %s",
                   GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
                   GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP,
-                  GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
+                  GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_E5_G, GJKEPA_E5_K, GJKEPA_E5_VCAP,
+                  GJKEPA_E5_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
                   GJKEPA_C1_K, GJKEPA_G0_MINW, GJKEPA_G1_MINW, GJKEPA_E0_MINW, GJKEPA_E1_MINW, GJKEPA_E2_MINW,
-                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH, GJKEPA_E0_LH,
-                  GJKEPA_E1_LH, GJKEPA_E2_LH, GJKEPA_E3_LH, GJKEPA_E4_LH, GJKEPA_C0_LH, GJKEPA_C1_LH, GJKEPA_SRC_HASH);
+                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_E5_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH,
+                  GJKEPA_E0_LH, GJKEPA_E1_LH, GJKEPA_E2_LH, GJKEPA_E3_LH, GJKEPA_E4_LH, GJKEPA_E5_LH, GJKEPA_C0_LH,
+                  GJKEPA_C1_LH, GJKEPA_SRC_HASH);
     return buf;
 }
 
@@ -782,10 +785,15 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
     if (rc) return rc;
     const auto t0 = std::chrono::steady_clock::now();
     auto next_check = t0 + std::chrono::microseconds(200);
+    bool yield = false;
     for (uint32_t spin = 1; __atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
         __builtin_ia32_pause();
+        // after twice a typical round trip, give the core away between polls: with more calling
+        // threads than cores, the threads whose answers have landed get to run
+        if (yield) std::this_thread::yield();
         if ((spin & 63u) == 0) {
             const auto now = std::chrono::steady_clock::now();
+            yield = now - t0 > std::chrono::microseconds(80);
             if (now >= next_check) {              // the grid may have drained under this request
                 if ((rc = service_ensure(sv, true)) != 0) return rc;
                 next_check = now + std::chrono::microseconds(200);

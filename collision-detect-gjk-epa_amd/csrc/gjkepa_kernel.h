@@ -89,6 +89,8 @@
 #ifndef GJKEPA_E2_REFILL
 #define GJKEPA_E2_REFILL 1      // C4 EPA tier 2 14.5 -> 13.7 ms, C5 40.5 -> 40.0 ms
 #endif
+// EPA tier 3: hulls of 129-256 vertices, first with a small polytope (one face row per lane, four
+// waves per SIMD); the ~16% of C4's large-hull pairs whose polytope outgrows it restart in tier 4
 #ifndef GJKEPA_E3_G
 #define GJKEPA_E3_G 64
 #endif
@@ -96,13 +98,13 @@
 #define GJKEPA_E3_K 4
 #endif
 #ifndef GJKEPA_E3_VCAP
-#define GJKEPA_E3_VCAP 104
+#define GJKEPA_E3_VCAP 40
 #endif
 #ifndef GJKEPA_E3_FCAP
-#define GJKEPA_E3_FCAP 208
+#define GJKEPA_E3_FCAP 64
 #endif
 #ifndef GJKEPA_E3_MINW
-#define GJKEPA_E3_MINW 2
+#define GJKEPA_E3_MINW 4
 #endif
 #ifndef GJKEPA_E4_G
 #define GJKEPA_E4_G 64
@@ -111,13 +113,28 @@
 #define GJKEPA_E4_K 4
 #endif
 #ifndef GJKEPA_E4_VCAP
-#define GJKEPA_E4_VCAP 208
+#define GJKEPA_E4_VCAP 104
 #endif
 #ifndef GJKEPA_E4_FCAP
-#define GJKEPA_E4_FCAP 416
+#define GJKEPA_E4_FCAP 208
 #endif
 #ifndef GJKEPA_E4_MINW
-#define GJKEPA_E4_MINW 1
+#define GJKEPA_E4_MINW 2
+#endif
+#ifndef GJKEPA_E5_G
+#define GJKEPA_E5_G 64
+#endif
+#ifndef GJKEPA_E5_K
+#define GJKEPA_E5_K 4
+#endif
+#ifndef GJKEPA_E5_VCAP
+#define GJKEPA_E5_VCAP 208
+#endif
+#ifndef GJKEPA_E5_FCAP
+#define GJKEPA_E5_FCAP 416
+#endif
+#ifndef GJKEPA_E5_MINW
+#define GJKEPA_E5_MINW 1
 #endif
 // one-wave query path (query_kernel, the resident query service): EPA's first polytope
 #ifndef GJKEPA_Q_VCAP
@@ -187,10 +204,13 @@
 #define GJKEPA_E2_LH 0
 #endif
 #ifndef GJKEPA_E3_LH
-#define GJKEPA_E3_LH 1             // 152 VGPRs: LDS-bound at 11 waves/CU (C4: EPA tier 3 100.4 -> 90.6 ms)
+#define GJKEPA_E3_LH 1
 #endif
 #ifndef GJKEPA_E4_LH
-#define GJKEPA_E4_LH 0
+#define GJKEPA_E4_LH 1             // 152 VGPRs: LDS-bound at 11 waves/CU (C4: EPA tier 3 100.4 -> 90.6 ms)
+#endif
+#ifndef GJKEPA_E5_LH
+#define GJKEPA_E5_LH 0
 #endif
 #ifndef GJKEPA_C0_LH
 #define GJKEPA_C0_LH 1             // contact features read the hull from LDS (A/B r3: C4 +5% with the one-pass dots)
@@ -202,7 +222,7 @@
 #define GJKEPA_CONTACT_OVERLAP 1    // each EPA tier's contact pass on a second stream, overlapping the later EPA tiers
 #endif
 #define GJKEPA_GJK_TIERS 2
-#define GJKEPA_EPA_TIERS 5
+#define GJKEPA_EPA_TIERS 6
 #define GJKEPA_CONTACT_TIERS 2
 
 // workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair

@@ -1720,13 +1720,19 @@ template <int G, typename T> DEV void store_record(void* out, int64_t pair, int 
 // hull capacity (vertices) of EPA tier t
 DEV constexpr int epa_hull_cap(int t) {
     return t == 0 ? GJKEPA_E0_G * GJKEPA_E0_K : t == 1 ? GJKEPA_E1_G * GJKEPA_E1_K : t == 2 ? GJKEPA_E2_G * GJKEPA_E2_K
-         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : GJKEPA_E4_G * GJKEPA_E4_K;
+         : t == 3 ? GJKEPA_E3_G * GJKEPA_E3_K : t == 4 ? GJKEPA_E4_G * GJKEPA_E4_K : GJKEPA_E5_G * GJKEPA_E5_K;
 }
-static_assert(GJKEPA_E4_G * GJKEPA_E4_K >= GJKEPA_MAX_HULL_VERTS, "the last EPA tier must hold every hull");
-// smallest EPA tier >= t0 whose hull capacity holds nmax vertices
-DEV int epa_tier_for(int nmax, int t0 = 0) {
+// polytope vertex capacity of EPA tier t
+DEV constexpr int epa_vcap(int t) {
+    return t == 0 ? GJKEPA_E0_VCAP : t == 1 ? GJKEPA_E1_VCAP : t == 2 ? GJKEPA_E2_VCAP : t == 3 ? GJKEPA_E3_VCAP
+         : t == 4 ? GJKEPA_E4_VCAP : GJKEPA_E5_VCAP;
+}
+static_assert(GJKEPA_E5_G * GJKEPA_E5_K >= GJKEPA_MAX_HULL_VERTS, "the last EPA tier must hold every hull");
+// smallest EPA tier >= t0 whose hull capacity holds nmax vertices and whose polytope capacity
+// exceeds vc (a pair deferred by a tier with polytope capacity vc skips tiers no larger)
+DEV int epa_tier_for(int nmax, int t0 = 0, int vc = 0) {
     for (int t = t0; t < GJKEPA_EPA_TIERS - 1; ++t)
-        if (nmax <= epa_hull_cap(t)) return t;
+        if (nmax <= epa_hull_cap(t) && epa_vcap(t) > vc) return t;
     return GJKEPA_EPA_TIERS - 1;
 }
 
@@ -2001,7 +2007,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
         const uint32_t diag = (gjk_it & 0xffu) | de;
         uint8_t next = 0;
         if (r == ST_DEFER && a.next_code >= 0) {   // next tier that holds the hulls
-            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0));
+            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
         } else if (r == 0) {
             // park depth, normal (record fields 0..3) and diag; the contact tier finishes the record
             T* rec = reinterpret_cast<T*>(slot);
@@ -2095,7 +2101,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
         const uint32_t diag = (gjk_it & 0xffu) | ((uint32_t)(S.iters & 0xff) << 8) | ((uint32_t)(S.nf & 0xffff) << 16);
         uint8_t next = 0;
         if (r == ST_DEFER && a.next_code >= 0) {
-            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0));
+            next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
         } else if (r == 0) {
             T* rec = reinterpret_cast<T*>(slot);
             if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
@@ -2177,9 +2183,9 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
 // costs no tier chain.  Tuned for the latency of one pair on an otherwise idle wave: the hull
 // register depth K (64K vertices per hull) is picked per pair from its larger hull, and EPA first
 // runs with a small polytope (GJKEPA_Q_VCAP / GJKEPA_Q_FCAP: one face row per lane) and only on
-// overflow restarts from the GJK simplex with EPA tier 4's polytope, as the tier chain's deferral
+// overflow restarts from the GJK simplex with the last EPA tier's polytope, as the tier chain's deferral
 // does.  Same device functions as the tier kernels, so the records are the chain's bit for bit.
-template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, true>;
+template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEPA_E5_VCAP, GJKEPA_E5_FCAP, true>;
 template <typename TIn, typename T, int K> using QLdsS = Lds<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, true>;
 template <typename TIn, typename T, int K>
 DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
@@ -2216,8 +2222,8 @@ DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, co
     uint32_t de = 0;
     r = epa_phase(c, kc, depth, n, de);
     __builtin_amdgcn_wave_barrier();
-    if (r == ST_DEFER) {                                 // small polytope full: tier 4's from the simplex
-        Ctx<T, TIn, 64, K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, 2> cb{*reinterpret_cast<QLds<TIn, T, K>*>(smem), grp};
+    if (r == ST_DEFER) {                                 // small polytope full: the last tier's from the simplex
+        Ctx<T, TIn, 64, K, GJKEPA_E5_VCAP, GJKEPA_E5_FCAP, 2> cb{*reinterpret_cast<QLds<TIn, T, K>*>(smem), grp};
         cb.na = na;
         cb.nb = nb;
         cb.vmax_a = c.vmax_a;
@@ -2485,7 +2491,8 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
         case 1: return launch_epa<TIn, T, EPA_ARGS(1), GJKEPA_E1_REFILL>(a, s);
         case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL>(a, s);
         case 3: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
-        default: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
+        case 4: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
+        default: return launch_epa<TIn, T, EPA_ARGS(5)>(a, s);
     }
 }
 

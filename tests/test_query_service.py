@@ -2,7 +2,7 @@
 answers single-pair calls (the reference's `CALL GJKEPA`, GCLIB_GJKEPA.f90:39-52) from host-mapped
 request slots.  Every record must be the oracle's bit for bit:
   - hulls of 4..256 vertices (the three hull register depths of the one-wave path) and deep
-    penetrations whose polytope outgrows the small first polytope (the restart with EPA tier 4's);
+    penetrations whose polytope outgrows the small first polytope (the restart with the last EPA tier's);
   - across the grid's idle drain and relaunch;
   - with more concurrent callers than request slots (the rest take the combining path)."""
 import concurrent.futures as cf
