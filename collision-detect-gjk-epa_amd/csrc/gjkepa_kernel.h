@@ -165,6 +165,12 @@
 #ifndef GJKEPA_EPA_SEED
 #define GJKEPA_EPA_SEED 1           // refill tiers: a fresh pair's iteration 1 joins the common support step (epa_seed)
 #endif
+#ifndef GJKEPA_GJK_META
+#define GJKEPA_GJK_META 1           // GJK tiers load every routed pair's hull counts / offsets once per chunk (0: per pair, A/B)
+#endif
+#ifndef GJKEPA_CONTACT_META
+#define GJKEPA_CONTACT_META 1       // contact tiers load every routed pair's hull counts / offsets once per chunk (0: per pair, A/B)
+#endif
 #ifndef GJKEPA_EPA_PLACE
 #define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
 #endif

@@ -1742,10 +1742,27 @@ DEV int epa_tier_for(int nmax, int t0 = 0, int vc = 0) {
 // pairs claim long runs so the scan is not bound by atomics on one address.  Inside a chunk, the wave ballots the pairs whose route byte matches this
 // launch (one coalesced byte load) and hands them to its 64/G groups in pair order, one per group
 // per round.  `route_code` < 0: every pair.  F(pair) runs for each pair the calling group receives.
-template <int G, typename F>
-DEV void groups_take(const Grp<G>& grp, int64_t p0, uint64_t m, F&& f) {
+// META: the pair metadata the callee needs first (hull counts and offsets) is loaded for every routed
+// pair of the chunk at once (lane l: pair p0 + l) and handed to each group with ds_bpermute, so a
+// round waits on one level of loads (the hulls) instead of three (pair -> hull -> vertices).
+struct PairMeta { int na, nb; int64_t oa, ob; };
+DEV int64_t shfl64(int64_t v, int src) {
+    const int lo = __shfl((int)(uint32_t)(uint64_t)v, src), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int G, bool META = false, typename F>
+DEV void groups_take(const Grp<G>& grp, int64_t p0, uint64_t m, const int32_t* pairs, const int32_t* cnt,
+                     const int64_t* off, F&& f) {
     constexpr int GPW = 64 / G;
     const int gid = grp.lane / G;
+    PairMeta mine{0, 0, 0, 0};
+    if constexpr (META) {
+        if ((m >> grp.lane) & 1ull) {
+            const int64_t p = p0 + grp.lane;
+            const int32_t ha = pairs[2 * p], hb = pairs[2 * p + 1];
+            mine.na = cnt[ha]; mine.nb = cnt[hb]; mine.oa = off[ha]; mine.ob = off[hb];
+        }
+    }
     while (m) {
         // group g takes the g-th lowest set bit of m
         uint64_t mm = m;
@@ -1753,7 +1770,14 @@ DEV void groups_take(const Grp<G>& grp, int64_t p0, uint64_t m, F&& f) {
         const bool active = mm != 0;
         const int bit = active ? (int)__builtin_ctzll(mm) : 0;
         for (int j = 0; j < GPW && m; ++j) m &= m - 1;   // consume this round's GPW matches
-        if (active) f(p0 + bit);
+        if constexpr (META) {
+            PairMeta pm;
+            pm.na = __shfl(mine.na, bit); pm.nb = __shfl(mine.nb, bit);
+            pm.oa = shfl64(mine.oa, bit); pm.ob = shfl64(mine.ob, bit);
+            if (active) f(p0 + bit, pm);
+        } else {
+            if (active) f(p0 + bit);
+        }
     }
 }
 // 16-bit mask of this lane's 16 route bytes equal to code
@@ -1815,9 +1839,10 @@ DEV int pick_claim(const uint32_t* tally, int route_code, int64_t n_pairs, int c
     return (int64_t)mine * 16 >= n_pairs ? 1 : claim;
 }
 
-template <int G, typename F>
+template <int G, bool META = false, typename F>
 DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t* __restrict__ route, int route_code,
-                              uint32_t* ctr, int claim, bool unit_grid, F&& f) {
+                              uint32_t* ctr, int claim, bool unit_grid, F&& f, const int32_t* pairs = nullptr,
+                              const int32_t* cnt = nullptr, const int64_t* off = nullptr) {
     // the first unit of workgroup b is unit b; later units come from the counter (offset by the
     // grid), so a launch with fewer units than workgroups issues no atomics at all.  unit_grid: the
     // launch has one workgroup per 64-pair chunk (dense launches only): a workgroup takes its own
@@ -1831,7 +1856,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
             const int len = n_pairs - p0 < 64 ? (int)(n_pairs - p0) : 64;
             const uint64_t m = route_code < 0 ? (len >= 64 ? ~0ull : ((1ull << len) - 1ull))
                                               : __ballot(grp.lane < len && (int)route[p0 + grp.lane] == route_code);
-            groups_take(grp, p0, m, f);
+            groups_take<G, META>(grp, p0, m, pairs, cnt, off, f);
         }
         return;
     }
@@ -1851,7 +1876,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
                 const int64_t p = p0 + grp.lane;
                 m = __ballot(grp.lane < len && (int)route[p] == route_code);
             }
-            groups_take(grp, p0, m, f);
+            groups_take<G, META>(grp, p0, m, pairs, cnt, off, f);
             u = (int64_t)__builtin_amdgcn_readfirstlane(next);
         }
         return;
@@ -1880,7 +1905,7 @@ DEV void for_each_routed_pair(const Grp<G>& grp, int64_t n_pairs, const uint8_t*
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 m |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mine, 4 * j + i) << (16 * i);
-            groups_take(grp, run * 1024 + 64 * j, m, f);
+            groups_take<G, META>(grp, run * 1024 + 64 * j, m, pairs, cnt, off, f);
         }
     }
 }
@@ -1903,11 +1928,10 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, [&](int64_t pair) {
+    auto body = [&](int64_t pair, const PairMeta& pm) {
         GK_STAMP(SG_ROUTE);
         Ctx<T, TIn, G, K, 0, 0, LH> c{L, grp};
-        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
-        const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
+        const int na = grp.uni(pm.na), nb = grp.uni(pm.nb);
         T o13[13];
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
@@ -1920,7 +1944,7 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         } else {
             c.na = na;
             c.nb = nb;
-            const bool bad_in = load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+            const bool bad_in = load_hulls(c, verts + pm.oa, verts + pm.ob);
             GK_STAMP(SG_LOAD);
             if (bad_in) {
                 store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
@@ -1958,7 +1982,16 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         if (gl == 0) { a.route[pair] = next; tally_route(next); }
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SG_STORE);
+    };
+#if GJKEPA_GJK_META
+    for_each_routed_pair<G, true>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, body, a.pairs, a.hull_cnt,
+                                  a.hull_off);
+#else
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, [&](int64_t pair) {
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        body(pair, PairMeta{a.hull_cnt[ha], a.hull_cnt[hb], a.hull_off[ha], a.hull_off[hb]});
     });
+#endif
     GK_STAMP(SG_ROUTE);
     tally_end(a.tally);
     GK_STAMP_END();
@@ -2365,17 +2398,16 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
     if (tier_empty(a.tally, a.route_code)) return;
     tally_begin();
     const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
-    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, a.grid == GJKEPA_GRID_UNITS, [&](int64_t pair) {
+    auto body = [&](int64_t pair, const PairMeta& pm) {
         GK_STAMP(SC_ROUTE);
         Ctx<T, TIn, G, K, 0, 1, LH> c{L, grp};
-        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
-        c.na = grp.uni(a.hull_cnt[ha]);
-        c.nb = grp.uni(a.hull_cnt[hb]);
+        c.na = grp.uni(pm.na);
+        c.nb = grp.uni(pm.nb);
         const T* rec = reinterpret_cast<const T*>(a.out) + pair * 16;     // 16 T fields per record
         const T depth = rec[0];
         const V3<T> n = vmk<T>(rec[1], rec[2], rec[3]);
         const uint32_t diag = reinterpret_cast<const uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + (sizeof(T) == 8 ? 27 : 14)];
-        load_hulls(c, verts + a.hull_off[ha], verts + a.hull_off[hb]);
+        load_hulls(c, verts + pm.oa, verts + pm.ob);
         GK_STAMP(SC_LOAD);
         T o13[13];
 #ifdef GJKEPA_DIAG_NO_CONTACT   // timing ablation only
@@ -2396,7 +2428,16 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
         if (gl == 0) a.route[pair] = 0;
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SC_STORE);
+    };
+#if GJKEPA_CONTACT_META
+    for_each_routed_pair<G, true>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, a.grid == GJKEPA_GRID_UNITS, body,
+                                  a.pairs, a.hull_cnt, a.hull_off);
+#else
+    for_each_routed_pair<G>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, a.grid == GJKEPA_GRID_UNITS, [&](int64_t pair) {
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        body(pair, PairMeta{a.hull_cnt[ha], a.hull_cnt[hb], a.hull_off[ha], a.hull_off[hb]});
     });
+#endif
     GK_STAMP(SC_ROUTE);
     tally_end(a.tally);
     GK_STAMP_END();
