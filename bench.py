@@ -97,6 +97,68 @@ def host_cpus() -> dict:
             "omp_num_threads": env or None}
 
 
+def verify_exchange(result, args, ex, comm, dist, world, rank, n, prec, rec_bytes, kern_ms_local, cfg, stream):
+    """N > 1, after the timed region: the record exchange checks itself.
+
+    - consistency: every rank hashes each rank's slot of its gathered buffer (last step); rank s's own
+      slot holds what its kernels wrote (the gather runs in place), so every rank's hash of slot s must
+      equal rank s's own hash of it;
+    - parity: rank 0 re-runs a subsample of every shard through the oracle (fp64 compute) and compares
+      it byte for byte with that shard's slot of its gathered buffer;
+    - timing: per-rank kernel ms (HIP events on the launch stream, mean per step) and the time of one
+      more stand-alone all-gather of the same buffer (events on the exchange stream; host clock for gloo).
+    """
+    import hashlib
+    import time as _t
+
+    import torch
+    gath = ex.last_gathered.cpu().numpy()
+    slot = n * rec_bytes
+    mine = [hashlib.sha256(gath[s * slot:(s + 1) * slot].tobytes()).hexdigest()[:16] for s in range(world)]
+    allh = [None] * world
+    dist.all_gather_object(allh, mine)
+    consistent = all(allh[r][s] == allh[s][s] for r in range(world) for s in range(world))
+    # one more gather of the same buffer, timed
+    b = ex.cur
+    if comm is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(ex.stream)
+        comm.allgather_records(prec, ex.local[b].data_ptr(), ex.gathered[b].data_ptr(), ex.count, ex.stream.cuda_stream)
+        e1.record(ex.stream)
+        e1.synchronize()
+        gather_ms = e0.elapsed_time(e1)
+    else:
+        t = _t.perf_counter()
+        g = torch.empty(ex.gathered[b].numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(g, ex.local[b].cpu(), group=ex.group)
+        ex.gathered[b].copy_(g)
+        torch.cuda.synchronize()
+        gather_ms = 1e3 * (_t.perf_counter() - t)
+    per = [None] * world
+    dist.all_gather_object(per, {"rank": rank, "kernel_ms": round(kern_ms_local, 4), "gather_ms": round(gather_ms, 4),
+                                 "slot_sha16": mine[rank]})
+    ps = {"gather_consistent": bool(consistent), "shards": world}
+    if rank == 0 and prec == gjkepa.PREC_F64 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker only
+        nmin, nmax, rmax = cfg
+        m = min(n, args.cpu_sample or 8192)
+        threads = host_cpus()["usable"]
+        eq_total, bad = 0, 0
+        for s in range(world):
+            first_s, _ = shard.shard_range(n * world, world, s)
+            sub = gjkepa.synth_pairs(SEED, m, nmin, nmax, rmax, first_pair=first_s, dtype=np.float32)
+            ref = np.frombuffer(oracle.gjkepa_batch(sub, args.version, 1.0, threads).tobytes(), np.uint8).reshape(m, -1)
+            got = gath[s * slot:s * slot + m * rec_bytes].reshape(m, -1)
+            eqr = (got == ref).all(axis=1)
+            eq_total += int(eqr.sum())
+            bad += int((~eqr).sum())
+        ps.update({"pairs": m * world, "pairs_per_shard": m, "bitexact_records": eq_total / (m * world),
+                   "all_equal": bad == 0 and consistent, "against": "oracle, every shard's slot of rank 0's gathered buffer"})
+    result["parity_sample"] = ps
+    result["per_rank"] = per
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,6 +262,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
+    kern_ms_local = kern_ms
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -333,6 +396,10 @@ def main():
             gjkepa.gjkepa_batch(pool, args.version, 1.0, precision=prec)
         result["host_api"] = {"value": round(2 * n / (time.perf_counter() - t) / 1e6, 3), "unit": "M queries/s",
                               "note": "gjkepa_batch on host buffers, PCIe transfers included"}
+
+    if dist and ex is not None:
+        verify_exchange(result, args, ex, comm, dist, world, rank, n, prec, rec_bytes, kern_ms_local,
+                        (nmin, nmax, rmax), stream)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

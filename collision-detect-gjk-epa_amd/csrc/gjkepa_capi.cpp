@@ -427,6 +427,7 @@ int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int3
                         const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
                         const int32_t* pairs, int64_t n_pairs, void* out, void* workspace,
                         int64_t workspace_bytes, void* stream) {
+    const gjkepa_internal::Range range_("gjkepa_batch_device (chain enqueue)");
     if (n_pairs < 0 || !valid_enums(vert_dtype, precision)) return fail(GJKEPA_E_ARG, "bad n_pairs/dtype/precision");
     if (n_pairs > 0 && (!verts || !hull_off || !hull_cnt || !pairs || !out || !workspace))
         return fail(GJKEPA_E_ARG, "null pointer");
@@ -439,6 +440,7 @@ int gjkepa_batch_warm_device(int32_t version, double tol_ff, int32_t vert_dtype,
                              const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
                              const int32_t* pairs, int64_t n_pairs, void* out, void* workspace,
                              int64_t workspace_bytes, uint32_t* warm, void* stream) {
+    const gjkepa_internal::Range range_("gjkepa_batch_warm_device (chain enqueue)");
     if (n_pairs < 0 || !valid_enums(vert_dtype, precision)) return fail(GJKEPA_E_ARG, "bad n_pairs/dtype/precision");
     if (n_pairs > 0 && (!verts || !hull_off || !hull_cnt || !pairs || !out || !workspace || !warm))
         return fail(GJKEPA_E_ARG, "null pointer");
@@ -451,6 +453,7 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
                  const void* verts, int64_t n_vert_scalars, const int64_t* hull_off,
                  const int32_t* hull_cnt, int64_t n_hulls, const int32_t* pairs, int64_t n_pairs,
                  void* out, int32_t device) {
+    const gjkepa_internal::Range range_("gjkepa_batch (H2D, chain, D2H)");
     if (n_pairs < 0 || n_hulls < 0 || n_vert_scalars < 0 || !valid_enums(vert_dtype, precision))
         return fail(GJKEPA_E_ARG, "bad sizes/dtype/precision");
     if (n_pairs == 0) return 0;
@@ -619,6 +622,11 @@ void run_queries(std::vector<Query*>& qs, int device) {
 #ifndef GJKEPA_SVC_IDLE_US
 #define GJKEPA_SVC_IDLE_US 2000
 #endif
+// longest residency of one grid, even under steady traffic: work that a later stream of the process
+// puts on the grid's hardware queue waits at most this long (plus one call) behind it
+#ifndef GJKEPA_SVC_LIFE_US
+#define GJKEPA_SVC_LIFE_US 20000
+#endif
 struct Service {
     std::mutex mu;                            // launches
     int device = 0, ok = 0;                   // ok: 1 ready, -1 unavailable
@@ -632,7 +640,7 @@ struct Service {
     std::atomic<uint32_t> gen{0};             // generation of the latest grid (0: none launched)
     std::atomic<uint64_t> free_slots{~0ull >> (64 - GJKEPA_SVC_SLOTS)};
     uint32_t seq[GJKEPA_SVC_SLOTS] = {};      // last posted sequence number, owned by the slot's holder
-    uint64_t idle_ticks = 0;
+    uint64_t idle_ticks = 0, life_ticks = 0;
 };
 static_assert(GJKEPA_SVC_SLOTS >= 1 && GJKEPA_SVC_SLOTS <= 64, "service slot bitmap");
 std::mutex g_svc_mu;
@@ -648,12 +656,17 @@ void service_shutdown() {                     // atexit: every wave sees its sto
     }
 }
 
+// on unless GJKEPA_QUERY_SERVICE=0; gjkepa_query_service_set() changes it at run time
+std::atomic<int> g_svc_on{-1};
 bool service_enabled() {
-    static const bool on = [] {
+    int on = g_svc_on.load(std::memory_order_relaxed);
+    if (on < 0) {
         const char* e = std::getenv("GJKEPA_QUERY_SERVICE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+        int want = !(e && e[0] == '0');
+        g_svc_on.compare_exchange_strong(on, want);
+        on = g_svc_on.load(std::memory_order_relaxed);
+    }
+    return on != 0;
 }
 
 // lock-free view of the services that are ready (per call: no mutex, no runtime query)
@@ -707,6 +720,7 @@ Service* service(int device) {
         hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || rate_khz <= 0)
         return nullptr;
     sv->idle_ticks = (uint64_t)rate_khz * GJKEPA_SVC_IDLE_US / 1000;
+    sv->life_ticks = (uint64_t)rate_khz * GJKEPA_SVC_LIFE_US / 1000;
     if (!g_svc_exit_hook) {
         std::atexit(service_shutdown);        // registered after the runtime's own: runs before its teardown
         g_svc_exit_hook = true;
@@ -739,7 +753,7 @@ int service_ensure(Service* sv, bool check_done) {
     if ((e = hipSetDevice(sv->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
     uint32_t ng = g1 + 1;
     if (ng == 0) ng = 1;
-    gjkepa_svc_args a{sv->dslots, sv->ctrl, sv->dclosing, ng, sv->idle_ticks};
+    gjkepa_svc_args a{sv->dslots, sv->ctrl, sv->dclosing, ng, sv->idle_ticks, sv->life_ticks};
     if ((e = gjkepa_launch_service(a, GJKEPA_SVC_SLOTS, sv->stream)) != hipSuccess) return hip_fail(e, "query service launch");
     if ((e = hipEventRecord(sv->ev, sv->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     sv->gen.store(ng, std::memory_order_release);
@@ -794,6 +808,8 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
         if ((spin & 63u) == 0) {
             const auto now = std::chrono::steady_clock::now();
             yield = now - t0 > std::chrono::microseconds(80);
+            // a grid that reached its idle or lifetime limit marks itself closing: relaunch at once
+            if ((rc = service_ensure(sv, false)) != 0) return rc;
             if (now >= next_check) {              // the grid may have drained under this request
                 if ((rc = service_ensure(sv, true)) != 0) return rc;
                 next_check = now + std::chrono::microseconds(200);
@@ -830,7 +846,10 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     if (slot < 0 && !device_state(device, &rc)) return rc;
     if (slot >= 0) {
         rc = service_run(sv, slot, version, tol_ff, p1, n1, p2, n2, &me.rec);
-        sv->free_slots.fetch_or(1ull << slot, std::memory_order_release);
+        // a request that may still be read by a late wave (no answer, or no grid launched) keeps its
+        // slot: the next holder would overwrite the hulls under that wave
+        if (rc == 0 || __atomic_load_n(&sv->slots[slot].done, __ATOMIC_ACQUIRE) == sv->seq[slot])
+            sv->free_slots.fetch_or(1ull << slot, std::memory_order_release);
         if (rc) return rc;
     } else {
     Combiner* cb = combiner(device);
@@ -886,6 +905,37 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     *penetration_depth = r.penetration_depth;
     if (status) *status = r.status;
     return 0;
+}
+
+int gjkepa_query_service_stop(int32_t device) {
+    std::vector<Service*> svs;
+    {
+        std::lock_guard<std::mutex> g(g_svc_mu);
+        for (size_t d = 0; d < g_svc.size(); ++d)
+            if (g_svc[d] && g_svc[d]->ok == 1 && (device < 0 || (size_t)device == d)) svs.push_back(g_svc[d]);
+    }
+    for (Service* sv : svs) {
+        std::lock_guard<std::mutex> g(sv->mu);    // no relaunch while the grid drains
+        const uint32_t gen = sv->gen.load(std::memory_order_acquire);
+        if (gen == 0) continue;
+        for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 1u, __ATOMIC_RELEASE);
+        // every wave answers the request its slot holds, sees its stop word and leaves
+        const hipError_t e = hipEventSynchronize(sv->ev);
+        for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(sv->closing, gen, __ATOMIC_RELEASE);   // the next call relaunches
+        if (e != hipSuccess) return hip_fail(e, "query service stop");
+    }
+    return 0;
+}
+
+int gjkepa_query_service_set(int32_t enabled) {
+    const bool prev = service_enabled();
+    g_svc_on.store(enabled ? 1 : 0, std::memory_order_relaxed);
+    if (!enabled) {
+        const int rc = gjkepa_query_service_stop(-1);
+        if (rc) return rc;
+    }
+    return prev ? 1 : 0;
 }
 
 // ---- batched convex hulls (include/gjkepa.h) ------------------------------
@@ -1097,6 +1147,7 @@ int gjkepa_collide(int32_t version, double tol_ff, int32_t vert_dtype, int32_t p
                    int64_t n_vert_scalars, const int64_t* hull_off, const int32_t* hull_cnt, int64_t n_hulls,
                    int32_t* pairs, void* out, int64_t max_contacts, int64_t* n_contacts, int64_t* n_candidates,
                    int32_t device) {
+    const gjkepa_internal::Range range_("gjkepa_collide (broad phase, chain, compaction)");
     if (n_hulls < 0 || max_contacts < 0 || n_vert_scalars < 0 || n_hulls > INT32_MAX - 1 || !valid_enums(vert_dtype, precision))
         return fail(GJKEPA_E_ARG, "bad sizes/dtype/precision");
     if (!n_contacts || (max_contacts > 0 && (!pairs || !out))) return fail(GJKEPA_E_ARG, "null pointer");

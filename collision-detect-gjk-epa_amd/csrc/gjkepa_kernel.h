@@ -355,5 +355,6 @@ struct gjkepa_svc_args {
     uint32_t* host_closing;          // device view of a host-mapped word: generation that is draining
     uint32_t gen;                    // this grid's generation (nonzero)
     uint64_t idle_ticks;             // wall-clock ticks without a request anywhere before the grid drains
+    uint64_t life_ticks;             // wall-clock ticks after which the grid drains even under traffic
 };
 hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStream_t s);

@@ -2329,6 +2329,7 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
     const uint32_t* hdr = &sl->req;
     uint32_t last = uni32(__hip_atomic_load(&sl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     uint64_t seen = wall_clock64();
+    const uint64_t born = seen;
     int empty = 0;
     for (;;) {
         // request line words 0, 1 (req, stop): relaxed system-scope reads (no cache invalidation
@@ -2369,7 +2370,9 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
         const uint64_t now = wall_clock64();
         const uint64_t g = __hip_atomic_load(&a.ctrl->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t act = g > seen ? g : seen;
-        if (now > act && now - act > a.idle_ticks) {
+        // idle for idle_ticks, or resident for life_ticks (bounds how long work queued behind the grid
+        // on a shared hardware queue can wait under steady traffic): drain; the next caller relaunches
+        if ((now > act && now - act > a.idle_ticks) || (now > born && now - born > a.life_ticks)) {
             if (grp.lane == 0) {
                 __hip_atomic_store(&a.ctrl->closing, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(a.host_closing, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

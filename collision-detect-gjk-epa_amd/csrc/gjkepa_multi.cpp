@@ -96,6 +96,7 @@ int gjkepa_batch_multi(int32_t version, double tol_ff, int32_t vert_dtype, int32
                        const void* verts, int64_t n_vert_scalars, const int64_t* hull_off,
                        const int32_t* hull_cnt, int64_t n_hulls, const int32_t* pairs, int64_t n_pairs,
                        void* out, const int32_t* devices, int32_t ndev) {
+    const gjkepa_internal::Range range_("gjkepa_batch_multi (shards on devices)");
     if (ndev < 1 || !devices) return set_error(GJKEPA_E_ARG, "empty device list");
     if (n_pairs < 0 || n_hulls < 0 || n_vert_scalars < 0) return set_error(GJKEPA_E_ARG, "bad sizes");
     const int rb = gjkepa_record_bytes(precision);
@@ -198,6 +199,7 @@ int gjkepa_comm_destroy(gjkepa_comm* comm) {
 
 int gjkepa_allgather_records_device(gjkepa_comm* comm, int32_t precision, const void* shard_records,
                                     void* all_records, int64_t count, void* stream) {
+    const gjkepa_internal::Range range_("gjkepa_allgather_records_device (RCCL all-gather enqueue)");
     const int rb = gjkepa_record_bytes(precision);
     if (!comm || rb < 0 || count < 0) return set_error(GJKEPA_E_ARG, "bad allgather arguments");
     if (count == 0) return 0;

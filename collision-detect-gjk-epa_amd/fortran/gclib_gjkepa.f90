@@ -14,6 +14,8 @@
 !                 the GPU: the list a caller's all-pairs GJKEPA loop reduces to.
 !   GJKEPA_COLLIDE  the whole all-pairs loop in one call: broad phase, GJKEPA on every candidate,
 !                 and only the colliding pairs returned with their GJKEPA outputs.
+!   GJKEPA_SERVICE_STOP  drain the resident grid that answers GJKEPA calls (include/gjkepa.h:
+!                 gjkepa_query_service_stop) before a device-wide synchronisation.
 !
 ! Only ISO_C_BINDING is used (no hipfort).  Hulls are REAL*8 p(n,3) exactly like the reference.
 !---------------------------------------------------------------------------------------------
@@ -22,6 +24,7 @@ MODULE GCLIB_GJKEPA
     IMPLICIT NONE
     PRIVATE
     PUBLIC :: GJKEPA, GJKEPA_BATCH, GJKEPA_LAST_STATUS, GJKEPA_SET_DEVICE, GJKEPA_BROADPHASE, GJKEPA_COLLIDE
+    PUBLIC :: GJKEPA_SERVICE_STOP
     PUBLIC :: GJKEPA_STATUS_OK, GJKEPA_STATUS_EPA_MAXITER, GJKEPA_STATUS_DEGENERATE
     PUBLIC :: GJKEPA_STATUS_BAD_VERSION, GJKEPA_STATUS_BAD_INPUT
 
@@ -114,6 +117,12 @@ MODULE GCLIB_GJKEPA
             INTEGER(C_INT) :: c_gjkepa_collide
         END FUNCTION c_gjkepa_collide
 
+        FUNCTION c_gjkepa_query_service_stop(dev) BIND(C, NAME="gjkepa_query_service_stop")
+            IMPORT :: C_INT32_T, C_INT
+            INTEGER(C_INT32_T), VALUE :: dev
+            INTEGER(C_INT) :: c_gjkepa_query_service_stop
+        END FUNCTION c_gjkepa_query_service_stop
+
         FUNCTION c_gjkepa_last_error() BIND(C, NAME="gjkepa_last_error")
             IMPORT :: C_PTR
             TYPE(C_PTR) :: c_gjkepa_last_error
@@ -158,6 +167,24 @@ CONTAINS
         nearest_points_ = RESHAPE(np, [2, 3])
         last_status = st
     END SUBROUTINE GJKEPA
+
+    !-----------------------------------------------------------------------------------------
+    ! GJKEPA_SERVICE_STOP — drain the grid that answers GJKEPA calls on the current device (all
+    ! devices with all_ = .TRUE.); later GJKEPA calls relaunch it.  rc_ (optional): 0 or GJKEPA_E_*.
+    !-----------------------------------------------------------------------------------------
+    SUBROUTINE GJKEPA_SERVICE_STOP(all_, rc_)
+        LOGICAL, INTENT(IN), OPTIONAL    :: all_
+        INTEGER*4, INTENT(OUT), OPTIONAL :: rc_
+        INTEGER(C_INT) :: rc
+        INTEGER(C_INT32_T) :: dev
+        dev = device
+        IF (PRESENT(all_)) THEN
+            IF (all_) dev = -1
+        END IF
+        rc = c_gjkepa_query_service_stop(dev)
+        IF (rc /= 0) CALL report(rc, "GJKEPA_SERVICE_STOP")
+        IF (PRESENT(rc_)) rc_ = rc
+    END SUBROUTINE GJKEPA_SERVICE_STOP
 
     !-----------------------------------------------------------------------------------------
     ! GJKEPA_BATCH — npairs queries in one submission.

@@ -35,6 +35,7 @@ EXPORTS = (
     "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
     "gjkepa_collide", "gjkepa_shard_range", "gjkepa_batch_multi", "gjkepa_comm_unique_id", "gjkepa_comm_init",
     "gjkepa_comm_destroy", "gjkepa_comm_backend", "gjkepa_allgather_records_device",
+    "gjkepa_query_service_stop", "gjkepa_query_service_set",
 )
 COMM_ID_BYTES = 128
 HULL_MAX_POINTS = 256
@@ -136,6 +137,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_comm_backend.restype = ctypes.c_char_p
     lib.gjkepa_allgather_records_device.argtypes = [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp]
     lib.gjkepa_allgather_records_device.restype = ctypes.c_int
+    lib.gjkepa_query_service_stop.argtypes = [c_i32]
+    lib.gjkepa_query_service_stop.restype = ctypes.c_int
+    lib.gjkepa_query_service_set.argtypes = [c_i32]
+    lib.gjkepa_query_service_set.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -179,6 +184,20 @@ def gjkepa(version: int, tol_ff: float, p1, p2, device: int = 0) -> Contact:
                           _ptr(hit), _ptr(typ), _ptr(npf), _ptr(nrm), _ptr(pt), _ptr(dep), _ptr(st), int(device))
     _check(rc, "gjkepa_query")
     return Contact(bool(hit[0]), int(typ[0]), npf.reshape(3, 2).T.copy(), nrm, pt, float(dep[0]), int(st[0]))
+
+
+def query_service_stop(device: int = -1) -> None:
+    """Drain the resident grid behind gjkepa() (include/gjkepa.h): call before a device-wide
+    synchronisation such as torch.cuda.synchronize() while single-pair calls may have run."""
+    _check(load().gjkepa_query_service_stop(int(device)), "gjkepa_query_service_stop")
+
+
+def query_service_set(enabled: bool) -> bool:
+    """Turn the resident query service on/off for later gjkepa() calls; returns the previous setting."""
+    rc = load().gjkepa_query_service_set(1 if enabled else 0)
+    if rc < 0:
+        _check(rc, "gjkepa_query_service_set")
+    return bool(rc)
 
 
 @dataclass

@@ -115,6 +115,26 @@ int gjkepa_query(int32_t version, double tol_ff,
                  double* collision_point, double* penetration_depth,
                  int32_t* status, int32_t device);
 
+/* ---- the resident query service behind gjkepa_query ------------------------------------------
+ * gjkepa_query posts each pair to a persistent grid of 64 one-wave workgroups (one per request slot
+ * in host-mapped memory) instead of launching kernels per call.  The grid runs on the library's own
+ * stream and leaves by itself once no call arrived for 2 ms, or after 20 ms of residency even under
+ * steady traffic (the next call relaunches it at once).  While it is resident:
+ *   - a device-wide synchronisation in the caller's process (hipDeviceSynchronize,
+ *     torch.cuda.synchronize() without a stream, a legacy default-stream sync) waits for the grid
+ *     to leave, i.e. up to 2 ms after the last call, or up to 20 ms while other threads keep calling;
+ *   - work the process enqueues on a stream that shares the grid's hardware queue (streams are
+ *     spread over GPU_MAX_HW_QUEUES queues) starts only after the grid leaves, within those bounds.
+ * Callers that synchronise the whole device, or want it idle, drain the grid first: */
+/* Drain the service grid of `device` (device < 0: every device) now; returns after it has left.
+ * Calls that arrive later relaunch it.  Returns 0 or GJKEPA_E_HIP. */
+int gjkepa_query_service_stop(int32_t device);
+/* Turn the service on (1) or off (0) for later gjkepa_query calls; off also drains every grid.  Off,
+ * single-pair calls of concurrent threads are combined into one batch launch (no resident grid).
+ * The initial setting is on unless the environment sets GJKEPA_QUERY_SERVICE=0.  Returns the
+ * previous setting (0/1) or a negative GJKEPA_E_* code. */
+int gjkepa_query_service_set(int32_t enabled);
+
 /* ---- batch over host buffers (blocking) ------------------------------------------------------
  * verts:     hull vertex pool, dtype `vert_dtype`, n_vert_scalars scalars in total.
  * hull_off:  [n_hulls] scalar offset of each hull's x[0] in `verts`.

@@ -94,3 +94,31 @@ def test_rccl_comm_world1_allgather():
     finally:
         comm.close()
     assert gjkepa.Comm.backend() != "unavailable"
+
+
+def test_two_rank_bench_verifies_its_exchange(tmp_path):
+    """bench.py at N = 2 (torch.distributed.run, one process per rank, gloo control plane, both ranks
+    on this box's one GPU, host-staged record exchange): each rank runs its shard through the library
+    on the GPU; the line it prints carries the exchange's own check (every rank holds every other
+    rank's records, rank 0's gathered buffer matches the oracle on a subsample of each shard) and the
+    per-rank kernel / gather times."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(root, "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--steps", "2", "--warmup", "1", "--pairs-per-gpu", "65536",
+           "--cpu-sample", "2048"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == 2 and r["config"]["total_pairs"] == 2 * 65536
+    ps = r["parity_sample"]
+    assert ps["gather_consistent"] and ps["all_equal"] and ps["bitexact_records"] == 1.0, ps
+    assert ps["pairs"] == 2 * 2048
+    assert sorted(x["rank"] for x in r["per_rank"]) == [0, 1]
+    assert all(x["kernel_ms"] > 0 and x["gather_ms"] > 0 for x in r["per_rank"])

@@ -1,8 +1,10 @@
 """gjkepa_query under the reference's call pattern: many threads calling the single-pair entry at
-once (`!$OMP PARALLEL DO ... CALL GJKEPA`, GCLIB_GJKEPA.f90:9, :16, :55-60).  The C-ABI combines
-the queued pairs of concurrent callers into one GPU batch per (version_, TOL_FF_); every caller
-must still get exactly its own record, bit for bit the oracle's, with versions and tolerances
-mixed across threads and pairs of different hull sizes in one batch."""
+once (`!$OMP PARALLEL DO ... CALL GJKEPA`, GCLIB_GJKEPA.f90:9, :16, :55-60).  Every test runs on both
+paths of the entry: the resident query service (default) and, with the service switched off
+(gjkepa_query_service_set(0)), the combiner, which batches the queued pairs of concurrent callers
+into one GPU launch per (version_, TOL_FF_).  Every caller must get exactly its own record, bit for
+bit the oracle's, with versions and tolerances (NaN included) mixed across threads and pairs of
+different hull sizes in one batch."""
 import concurrent.futures as cf
 
 import numpy as np
@@ -24,6 +26,19 @@ def _pairs(n, seed):
         b += d / np.linalg.norm(d) * rng.uniform(0, 2.5)
         out.append((int(1 + i % 3), (1.0, 1e-3)[i % 2], a, b))
     return out
+
+
+@pytest.fixture(params=["service", "combiner"], autouse=True)
+def query_path(request):
+    """Run the module's tests through the resident service and through the combiner."""
+    if "gpu" not in request.keywords:
+        yield request.param
+        return
+    prev = gjkepa.query_service_set(request.param == "service")
+    try:
+        yield request.param
+    finally:
+        gjkepa.query_service_set(prev)
 
 
 def _same(c, r):

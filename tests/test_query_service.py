@@ -6,6 +6,7 @@ request slots.  Every record must be the oracle's bit for bit:
   - across the grid's idle drain and relaunch;
   - with more concurrent callers than request slots (the rest take the combining path)."""
 import concurrent.futures as cf
+import threading
 import time
 
 import numpy as np
@@ -70,3 +71,87 @@ def test_service_bad_sizes(orc):
     big = np.random.default_rng(2).normal(size=(300, 3))
     c = gjkepa.gjkepa(2, 1.0, big, b)
     assert c.status == gjkepa.STATUS_BAD_INPUT and not c.collision
+
+
+def _traffic(stop_evt, qs, counter):
+    """One caller thread: single-pair calls in a loop until stop_evt is set."""
+    i = 0
+    while not stop_evt.is_set():
+        gjkepa.gjkepa(*qs[i % len(qs)])
+        i += 1
+    counter.append(i)
+
+
+@pytest.mark.gpu
+def test_stop_then_device_synchronize_returns_promptly(orc):
+    """gjkepa_query_service_stop drains the grid: a device-wide synchronisation right after it does
+    not wait for the service's idle timeout, and the next call relaunches the grid (include/gjkepa.h)."""
+    import torch
+    qs = _big_pairs(8, 31, 4, 40)
+    for q in qs:
+        gjkepa.gjkepa(*q)                  # grid resident now
+    t = time.perf_counter()
+    gjkepa.query_service_stop(0)
+    t_stop = time.perf_counter() - t
+    t = time.perf_counter()
+    torch.cuda.synchronize()
+    t_sync = time.perf_counter() - t
+    assert t_stop < 0.5, t_stop
+    assert t_sync < 0.0015, f"synchronize after stop took {t_sync * 1e3:.2f} ms (idle drain is 2 ms)"
+    got = [gjkepa.gjkepa(*q) for q in qs]  # relaunched
+    _check(orc, qs, got)
+    gjkepa.query_service_stop(-1)          # all devices; nothing running is fine too
+    gjkepa.query_service_stop(-1)
+
+
+@pytest.mark.gpu
+def test_synchronize_bounded_under_sustained_queries():
+    """Under steady single-pair traffic the grid never idles; its 20 ms residency bound still lets a
+    device-wide synchronisation return (it would otherwise wait until the traffic stops)."""
+    import torch
+    qs = _big_pairs(32, 41, 4, 40)
+    stop_evt, counts = threading.Event(), []
+    th = [threading.Thread(target=_traffic, args=(stop_evt, qs, counts)) for _ in range(4)]
+    for x in th:
+        x.start()
+    try:
+        time.sleep(0.1)
+        waits = []
+        for _ in range(5):
+            t = time.perf_counter()
+            torch.cuda.synchronize()
+            waits.append(time.perf_counter() - t)
+            time.sleep(0.05)
+    finally:
+        stop_evt.set()
+        for x in th:
+            x.join()
+    assert max(waits) < 0.25, waits
+    assert sum(counts) > 100
+
+
+@pytest.mark.gpu
+def test_batches_finish_beside_sustained_queries(orc):
+    """gjkepa_batch calls on the same device while other threads keep the service busy: every batch
+    finishes (the grid's residency bound) and its records are the oracle's."""
+    qs = _big_pairs(32, 43, 4, 40)
+    pool = gjkepa.synth_pairs(0x6A4B5C1D, 20000, 32, 32, 2.5)
+    ref = orc.gjkepa_batch(gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:2000]), 2, 1.0)
+    stop_evt, counts = threading.Event(), []
+    th = [threading.Thread(target=_traffic, args=(stop_evt, qs, counts)) for _ in range(8)]
+    for x in th:
+        x.start()
+    times = []
+    try:
+        time.sleep(0.05)
+        for _ in range(4):
+            t = time.perf_counter()
+            g = gjkepa.gjkepa_batch(pool, 2, 1.0, gjkepa.PREC_F64)
+            times.append(time.perf_counter() - t)
+            assert g[:2000].tobytes() == ref.tobytes()
+    finally:
+        stop_evt.set()
+        for x in th:
+            x.join()
+    assert max(times) < 1.0, times
+    assert sum(counts) > 100
