@@ -343,19 +343,13 @@ def main():
         torch.cuda.synchronize(dev)
         ms32 = s.elapsed_time(e) / args.steps
         r32 = np.frombuffer(out32.cpu().numpy().tobytes(), dtype=gjkepa.REC32)
-        # errors against the fp64 records of the same batch (byte-identical to the oracle: parity_sample)
-        both = (r32["collision"] != 0) & (recs["collision"] != 0) & (r32["status"] == 0) & (recs["status"] == 0)
-        d64 = recs["penetration_depth"][both].astype(np.float64)
-        derr = np.abs(r32["penetration_depth"][both].astype(np.float64) - d64) / np.maximum(np.abs(d64), 1e-9)
-        a, b = r32["collision_normal"][both].astype(np.float64), recs["collision_normal"][both].astype(np.float64)
-        cosang = np.sum(a * b, axis=1) / np.maximum(np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1), 1e-300)
-        ang = np.arccos(np.clip(cosang, -1.0, 1.0))
-        q = (lambda x, p: float(np.quantile(x, p)) if x.size else 0.0)
-        result["fp32_compute"] = {"value": round(n / (ms32 * 1e-3) / 1e6, 3), "unit": "M queries/s",
-                                  "hit_agreement_vs_f64": round(float((r32["collision"] == recs["collision"]).mean()), 6),
-                                  "depth_relerr_p999": q(derr, 0.999), "depth_relerr_max": float(derr.max()) if derr.size else 0.0,
-                                  "normal_angle_rad_p999": q(ang, 0.999),
-                                  "normal_angle_rad_max": float(ang.max()) if ang.size else 0.0}
+        # errors against the fp64 records of the same batch (byte-identical to the oracle: parity_sample),
+        # with the full-batch gate of tests/test_gpu_parity.py::test_fp32_tolerance_sweep (tools/fp32_metrics.py)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from fp32_metrics import fp32_report, passes
+        rep = fp32_report(pool, r32, recs)
+        result["fp32_compute"] = {"value": round(n / (ms32 * 1e-3) / 1e6, 3), "unit": "M queries/s", **rep,
+                                  "gate_passed": passes(rep)}
 
     # warm start: frames alternate between the batch and a copy with every hull B moved
     # by 1e-3; each frame's warm slots seed the next.  Cold = the same frames through batch_device.

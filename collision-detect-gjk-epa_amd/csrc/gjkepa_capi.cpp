@@ -225,7 +225,9 @@ constexpr int overlap_launches() {
         if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t);
     return n;
 }
-static_assert(overlap_launches() <= GJKEPA_WS_COUNTERS, "workspace launch counters");
+static_assert(overlap_launches() + 1 <= GJKEPA_WS_COUNTERS, "workspace launch counters (+1: the fp32 redo launch)");
+static_assert(GJKEPA_ROUTE_REDO < GJKEPA_WS_TALLY && GJKEPA_ROUTE_REDO > GJKEPA_ROUTE_CT(GJKEPA_EPA_TIERS - 1) + 1,
+              "redo route code");
 // The forked contact pass of EPA tier 0 (a dense launch) takes one workgroup per 64-pair chunk
 // instead of an occupancy-sized grid of looping workgroups: a workgroup leaves when its chunk is
 // done, so the EPA tiers launched beside the pass get wave slots as they free up instead of
@@ -331,6 +333,19 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         }
         return 0;
     };
+    // fp32 compute: the pairs whose fp32 answer was not certified, recomputed in fp64 (after every
+    // contact pass has joined the caller's stream; an empty launch returns at once)
+    auto redo = [&]() -> int {
+        if (precision != GJKEPA_PREC_F32) return 0;
+        a.route_code = GJKEPA_ROUTE_REDO;
+        a.next_code = -1;
+        a.ctr = ctr + launch++;
+        a.claim = kSparseClaim;
+        a.grid = 0;
+        a.guard = gjkepa_guard_of(a);
+        hipError_t er = gjkepa_launch_redo(vert_dtype, a, s);
+        return er == hipSuccess ? 0 : hip_fail(er, "fp32 redo launch");
+    };
     if (overlap) {
         std::lock_guard<std::mutex> lk(f->mu);
         constexpr int last = GJKEPA_EPA_TIERS - 1;
@@ -355,11 +370,12 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             if ((e = hipEventRecord(f->join[t], f->s2[t])) != hipSuccess || (e = hipStreamWaitEvent(s, f->join[t], 0)) != hipSuccess)
                 return hip_fail(e, "contact pass join");
         }
-        return 0;
+        return redo();
     }
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
         if ((rc = epa_tier(t))) return rc;
-    return contact_tiers(GJKEPA_ROUTE_CT0, GJKEPA_CONTACT_TIERS, s);
+    if ((rc = contact_tiers(GJKEPA_ROUTE_CT0, GJKEPA_CONTACT_TIERS, s))) return rc;
+    return redo();
 }
 
 // select `device` and create its stream on first use (caller holds d->mu)

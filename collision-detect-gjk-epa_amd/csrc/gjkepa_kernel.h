@@ -244,6 +244,10 @@
 #define GJKEPA_ROUTE_CT0 0x20       // + contact tier
 // with GJKEPA_CONTACT_OVERLAP, the pairs EPA tier t finishes go to contact tier c under code CT(t) + c
 #define GJKEPA_ROUTE_CT(t) (GJKEPA_ROUTE_CT0 + 2 * (t))
+// fp32 compute: pairs whose fp32 answer is not certified (EPA's MINLOC distance dropped or its final
+// support gap is open, or an fp32 error status) are recomputed whole in fp64 by the redo launch at
+// the end of the chain (gjkepa_kernel.hip "fp32 certificate")
+#define GJKEPA_ROUTE_REDO 0x2E
 
 // gjkepa_*_args::grid: > 0 explicit, 0 occupancy x CUs (looping workgroups), GJKEPA_GRID_UNITS one
 // workgroup per work unit
@@ -322,6 +326,9 @@ hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjke
 hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
 // contact tiers take the same argument block (route_code = GJKEPA_ROUTE_CT0 + tier; next_code unused)
 hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
+// fp32 chain's last launch: the pairs routed GJKEPA_ROUTE_REDO, one wave each, GJK + EPA + contact in
+// fp64, stored as fp32 records
+hipError_t gjkepa_launch_redo(int vert_dtype, const gjkepa_epa_args& a, hipStream_t s);
 // one-kernel path for small batches: one wave per pair (grid = n_pairs), GJK + EPA + contact features
 hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
 // the chain's counter / tally reset (n32 uint32 words from ws); a kernel node rather than a memset node

@@ -33,6 +33,23 @@
 namespace gk {
 
 constexpr int ST_DEFER = 100;   // internal: does not fit this tier
+constexpr int ST_REDO = 103;    // internal (fp32 compute): answer not certified, recompute in fp64
+
+// fp32 certificate.  An fp32 EPA can build an invalid polytope from inconsistent visibility decisions
+// on near-coplanar faces (the fp32 rounding of a sliver's normal), after which its MINLOC distance
+// drops and it may stop far from the penetration depth (C5: 20% low, normal off by 0.4 rad on one
+// pair in 2^20).  In exact arithmetic EPA's MINLOC distance never decreases (each polytope contains
+// the last) and at termination the support along the final normal lies on the final face, so the
+// fp32 path checks both: a drop of more than CERT_DROP * max(1, d) between iterations, or a support
+// gap h_M(n) - d above CERT_GAP * max(1, d) when EPA stops, sends the pair to the redo launch, which
+// recomputes it whole in fp64 (so do fp32 error statuses that fp64 may not share).  A certified
+// answer has d <= h_M(n) <= d + gap, and d cannot exceed the depth of the polytope it came from.
+template <typename T> DEV constexpr bool certify() { return sizeof(T) == 4; }
+// fp32 compute: an EPA / contact outcome the fp64 recomputation may answer differently
+template <typename T> DEV bool redo_status(int r, bool last_tier) {
+    if constexpr (!certify<T>()) return false;
+    return r == ST_REDO || r == GJKEPA_STATUS_EPA_MAXITER || r == GJKEPA_STATUS_DEGENERATE || (r == ST_DEFER && last_tier);
+}
 
 // GET_RANDOM_UNIT_VECTOR table (:1578-1689)
 __constant__ double kDirTab[100][3] = {
@@ -813,6 +830,7 @@ template <typename T, int R> struct EpaState {
     bool neg;                      //   DIST_PF_SIGN(O, face) < 0,
     int av;                        //   first vertex id
     bool unchanged;
+    T hsup;                        // fp32 certificate: support value along dir of the last support step
 };
 #define EPAST_T EpaState<T, (FC + G - 1) / G>
 
@@ -856,6 +874,7 @@ CTX_T DEV int epa_begin(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> 
     if (c.g.unib(dt <= -Tol<T>::ZO)) dir = vneg(dir);         // :910
     GK_STAMP(SE_IT1);
     const V3<T> sp = support(c, dir);                          // :914
+    if constexpr (certify<T>()) { S.minv = minv; S.hsup = dot(sp, dir); }
     const bool two = c.g.unib(fabs(minv) < Tol<T>::ZO);        // :935
     // unique polytope vertices (getHullMeshesVertex, :920) + new point(s) -> ids 0..m-1
     const bool u1 = !veq(s1, s0);
@@ -966,7 +985,11 @@ CTX_T DEV int epa_seed(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s
 CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     const V3<T> O = zero3<T>();
     const int F2 = S.nf;                                      // :956-969
+    const T prev = S.minv;
     face_argmin(c, S.F, S.minv, S.dir, S.neg, S.av);
+    if constexpr (certify<T>()) {                             // fp32 certificate: MINLOC never drops
+        if (c.g.unib(S.minv < prev - Tol<T>::CERT_DROP * (prev > T(1) ? prev : T(1)))) return ST_REDO;
+    }
     // dot(a1 - O, n) is -DIST_PF_SIGN(O, face) (exact negation; a zero's sign never matters here):
     // negative iff the face's signed distance is positive
     V3<T> dir2 = S.dir;
@@ -975,6 +998,9 @@ CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F, S.hw);   // unchanged hull: identical sorted lists
     else stop = S.F1 > F2;
     GK_STAMP(SE_TERM);
+    if constexpr (certify<T>()) {                             // fp32 certificate: closed support gap
+        if (stop && c.g.unib(S.hsup - S.minv > Tol<T>::CERT_GAP * (S.minv > T(1) ? S.minv : T(1)))) return ST_REDO;
+    }
     if (stop) { depth = S.minv; normal = dir2; return 0; }
     // ---- next iteration: same faces as this iteration's F2, so its MINLOC carries over
     S.iters = S.iters + 1;
@@ -998,6 +1024,7 @@ CTX_T DEV int epa_grow(CTX& c, EPAST_T& S, bool first) {
     const int gl = c.g.gl;
     const V3<T> dir = S.dir;
     const V3<T> sp = support(c, dir);                          // :914
+    if constexpr (certify<T>()) S.hsup = dot(sp, dir);
     GK_STAMP(SE_SUP);
     const bool two = c.g.unib(fabs(S.minv) < Tol<T>::ZO);      // :935
     if (two && !first) {                  // net face count of two insertions unknown: save now
@@ -1974,6 +2001,8 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                     next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(na > nb ? na : nb));
                 } else if (r == PH_MISS) {
                     store_record<G, T>(a.out, pair, gl, o13, 0, 0, 0, 0u);
+                } else if (certify<T>()) {                // fp32: GJK-phase error, recomputed in fp64
+                    next = GJKEPA_ROUTE_REDO;
                 } else {                                  // GJK-phase error (reference would STOP)
                     store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
                 }
@@ -2041,6 +2070,8 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
         uint8_t next = 0;
         if (r == ST_DEFER && a.next_code >= 0) {   // next tier that holds the hulls
             next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
+        } else if (redo_status<T>(r, a.next_code < 0)) {   // fp32: not certified, recomputed in fp64
+            next = GJKEPA_ROUTE_REDO;
         } else if (r == 0) {
             // park depth, normal (record fields 0..3) and diag; the contact tier finishes the record
             T* rec = reinterpret_cast<T*>(slot);
@@ -2135,6 +2166,8 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
         uint8_t next = 0;
         if (r == ST_DEFER && a.next_code >= 0) {
             next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
+        } else if (redo_status<T>(r, a.next_code < 0)) {   // fp32: not certified, recomputed in fp64
+            next = GJKEPA_ROUTE_REDO;
         } else if (r == 0) {
             T* rec = reinterpret_cast<T*>(slot);
             if (gl < 4) rec[gl] = gl == 0 ? depth : gl == 1 ? n.x : gl == 2 ? n.y : n.z;
@@ -2220,8 +2253,10 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
 // does.  Same device functions as the tier kernels, so the records are the chain's bit for bit.
 template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEPA_E5_VCAP, GJKEPA_E5_FCAP, true>;
 template <typename TIn, typename T, int K> using QLdsS = Lds<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, true>;
-template <typename TIn, typename T, int K>
-DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
+// RT: the record's field type (T, or float for the fp32 chain's fp64 redo).  Returns true when an fp32
+// answer is not certified (certify<T>(): nothing stored; the caller recomputes the pair in fp64).
+template <typename TIn, typename T, int K, typename RT = T>
+DEV bool query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
                       int version, T tol_ff, void* out, int64_t pair) {
     using LB = QLds<TIn, T, K>;
     using LS = QLdsS<TIn, T, K>;
@@ -2230,25 +2265,27 @@ DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, co
     const int gl = grp.gl;
     Ctx<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, 2> c{*reinterpret_cast<QLdsS<TIn, T, K>*>(smem), grp};
     T o13[13];
+    RT o[13];
 #pragma unroll
-    for (int i = 0; i < 13; ++i) o13[i] = T(0);
+    for (int i = 0; i < 13; ++i) { o13[i] = T(0); o[i] = RT(0); }
     c.na = na;
     c.nb = nb;
     if (load_hulls(c, pa, pb)) {
-        store_record<64, T>(out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
-        return;
+        store_record<64, RT>(out, pair, gl, o, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+        return false;
     }
     uint32_t kc[4];
     int gjk_it = 0;
     int r = gjk_phase(c, kc, gjk_it, GJKEPA_AXIS_REJECT != 0);
     __builtin_amdgcn_wave_barrier();
     if (r == PH_MISS) {
-        store_record<64, T>(out, pair, gl, o13, 0, 0, 0, 0u);
-        return;
+        store_record<64, RT>(out, pair, gl, o, 0, 0, 0, 0u);
+        return false;
     }
     if (r != PH_HIT) {                                   // GJK-phase error (reference would STOP)
-        store_record<64, T>(out, pair, gl, o13, 1, 0, r, (uint32_t)(gjk_it & 0xff));
-        return;
+        if (certify<T>()) return true;
+        store_record<64, RT>(out, pair, gl, o, 1, 0, r, (uint32_t)(gjk_it & 0xff));
+        return false;
     }
     T depth;
     V3<T> n;
@@ -2264,38 +2301,46 @@ DEV void query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, co
         r = epa_phase(cb, kc, depth, n, de);
         __builtin_amdgcn_wave_barrier();
     }
+    if (redo_status<T>(r, true)) return true;
     const uint32_t diag = ((uint32_t)gjk_it & 0xffu) | de;
     if (r != 0) {                                        // last tier out of capacity: DEGENERATE
-        store_record<64, T>(out, pair, gl, o13, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
-        return;
+        store_record<64, RT>(out, pair, gl, o, 1, 0, r == ST_DEFER ? GJKEPA_STATUS_DEGENERATE : r, diag);
+        return false;
     }
     r = contact_phase(c, depth, n, version, tol_ff, o13);
     __builtin_amdgcn_wave_barrier();
     if (r < 0) {
-        store_record<64, T>(out, pair, gl, o13, 1, -r, 0, diag);
-    } else {
 #pragma unroll
-        for (int i = 0; i < 13; ++i) o13[i] = T(0);
-        store_record<64, T>(out, pair, gl, o13, 1, 0, r, diag);
+        for (int i = 0; i < 13; ++i) o[i] = (RT)o13[i];
+        store_record<64, RT>(out, pair, gl, o, 1, -r, 0, diag);
+    } else {
+        if (redo_status<T>(r, false)) return true;
+        store_record<64, RT>(out, pair, gl, o, 1, 0, r, diag);
     }
+    return false;
 }
 
-// one pair on this wave: hull depth from the larger hull; bad sizes answered BAD_INPUT
-template <typename TIn, typename T>
+// one pair on this wave: hull depth from the larger hull; bad sizes answered BAD_INPUT.  An fp32 answer
+// that is not certified is recomputed here in fp64 (records stay fp32): the redo launch's work, inline.
+template <typename TIn, typename T, typename RT = T>
 DEV void query_pair(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
                     int version, T tol_ff, void* out, int64_t pair) {
     const int nmax = na > nb ? na : nb;
+    bool redo = false;
     if (na < 1 || nb < 1 || nmax > GJKEPA_MAX_HULL_VERTS) {
-        T o13[13];
+        RT o[13];
 #pragma unroll
-        for (int i = 0; i < 13; ++i) o13[i] = T(0);
-        store_record<64, T>(out, pair, grp.gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
+        for (int i = 0; i < 13; ++i) o[i] = RT(0);
+        store_record<64, RT>(out, pair, grp.gl, o, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
     } else if (nmax <= 64) {
-        query_pair_k<TIn, T, 1>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+        redo = query_pair_k<TIn, T, 1, RT>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
     } else if (nmax <= 128) {
-        query_pair_k<TIn, T, 2>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+        redo = query_pair_k<TIn, T, 2, RT>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
     } else {
-        query_pair_k<TIn, T, GJKEPA_MAX_HULL_VERTS / 64>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+        redo = query_pair_k<TIn, T, GJKEPA_MAX_HULL_VERTS / 64, RT>(smem, grp, pa, pb, na, nb, version, tol_ff, out, pair);
+    }
+    if constexpr (certify<T>()) {
+        if (redo) query_pair<TIn, double, RT>(smem, grp, pa, pb, na, nb, version, (double)tol_ff, out, pair);
     }
 }
 
@@ -2311,6 +2356,28 @@ __global__ __launch_bounds__(64, 1) void query_kernel(const gjkepa_epa_args a) {
     const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
     query_pair<TIn, T>(smem, grp, verts + a.hull_off[ha], verts + a.hull_off[hb], na, nb, a.version, (T)a.tol_ff,
                        a.out, pair);
+}
+
+// The fp32 chain's last launch: every pair routed GJKEPA_ROUTE_REDO (an fp32 answer that was not
+// certified, or an fp32 error status) recomputed whole (GJK, EPA, contact features) in fp64 by one
+// wave, stored as its fp32 record: the fp64 path's record rounded to fp32.  Few pairs (about 1 in
+// 10^4 on C2 / C5), so one wave per pair and the sparse claim.
+template <typename TIn>
+__global__ __launch_bounds__(64, 1) void redo_kernel(const gjkepa_epa_args a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const Grp<64> grp;
+    const TIn* verts = (const TIn*)a.verts;
+    GK_GUARD(7, a.route_code);
+    if (tier_empty(a.tally, a.route_code)) return;
+    const int claim = pick_claim(a.tally, a.route_code, a.n_pairs, a.claim);
+    for_each_routed_pair<64>(grp, a.n_pairs, a.route, a.route_code, a.ctr, claim, false, [&](int64_t pair) {
+        const int32_t ha = a.pairs[2 * pair], hb = a.pairs[2 * pair + 1];
+        const int na = grp.uni(a.hull_cnt[ha]), nb = grp.uni(a.hull_cnt[hb]);
+        query_pair<TIn, double, float>(smem, grp, verts + a.hull_off[ha], verts + a.hull_off[hb], na, nb, a.version,
+                                       a.tol_ff, a.out, pair);
+        if (grp.gl == 0) a.route[pair] = 0;
+        __builtin_amdgcn_wave_barrier();
+    });
 }
 
 // Resident query service (gjkepa_query, include/gjkepa.h): wave w serves request slot w of
@@ -2421,14 +2488,17 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
         const int r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
 #endif
         __builtin_amdgcn_wave_barrier();
+        uint8_t next = 0;
         if (r < 0) {
             store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
+        } else if (redo_status<T>(r, false)) {   // fp32: contact-phase error, recomputed in fp64
+            next = GJKEPA_ROUTE_REDO;
         } else {                 // error status: outputs zero, collision = 1
 #pragma unroll
             for (int i = 0; i < 13; ++i) o13[i] = T(0);
             store_record<G, T>(a.out, pair, gl, o13, 1, 0, r, diag);
         }
-        if (gl == 0) a.route[pair] = 0;
+        if (gl == 0) { a.route[pair] = next; if (next) tally_route(next); }
         __builtin_amdgcn_wave_barrier();
         GK_STAMP(SC_STORE);
     };
@@ -2580,10 +2650,21 @@ hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStrea
 }
 
 template <typename TIn, typename T> hipError_t launch_query(const gjkepa_epa_args& a, hipStream_t s) {
-    using L_t = gk::QLds<TIn, T, GJKEPA_MAX_HULL_VERTS / 64>;
+    // an fp32 query recomputes an uncertified pair in fp64 in place: room for the fp64 image
+    using L_t = gk::QLds<TIn, double, GJKEPA_MAX_HULL_VERTS / 64>;
     auto kfn = gk::query_kernel<TIn, T>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)a.n_pairs), dim3(64), sizeof(L_t), s, a);
     return hipGetLastError();
+}
+template <typename TIn> hipError_t launch_redo(const gjkepa_epa_args& a, hipStream_t s) {
+    using L_t = gk::QLds<TIn, double, GJKEPA_MAX_HULL_VERTS / 64>;
+    auto kfn = gk::redo_kernel<TIn>;
+    const int grid = grid_cap<64>(a.n_pairs, grid_for(kfn, sizeof(L_t), a.num_cus, a.grid));
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), sizeof(L_t), s, a);
+    return hipGetLastError();
+}
+hipError_t gjkepa_launch_redo(int vert_dtype, const gjkepa_epa_args& a, hipStream_t s) {
+    return vert_dtype == GJKEPA_DTYPE_F32 ? launch_redo<float>(a, s) : launch_redo<double>(a, s);
 }
 hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
     if (vert_dtype == GJKEPA_DTYPE_F32)

@@ -34,6 +34,10 @@ template <> struct Tol<float> {              // fp32 throughput path: tolerances
     static constexpr float POS = 1.0e-15f;
     static constexpr float HULL = 2.0e-6f;
     static constexpr float BIG = FLT_MAX;
+    // fp32 certificate (gjkepa_kernel.hip, epa_close): largest drop of the polytope's MINLOC distance
+    // between iterations, and largest support gap h_M(n) - depth at termination, relative to max(1, depth)
+    static constexpr float CERT_DROP = 1.0e-5f;
+    static constexpr float CERT_GAP = 1.0e-5f;
 };
 
 DEV double tsqrt(double x) { return ::sqrt(x); }

@@ -31,10 +31,24 @@
 #endif
 
 /* ---- tolerances ---------------------------------------------------- */
+#ifndef ORC_F32
 #define TOL_PT   1.0e-8   /* coincidence / coplanar / collinear / on-plane / EPA convergence */
-#define TOL_Z    1.0e-12  /* UTZVEC / UNINML / DIST_PF_SIGN zero, EPA orientation, origin-on-face */
+#define TOL_Z    1.0e-12  /* UTZVEC / UNINML / DIST_PF_SIGN zero */
+#define TOL_ZO   1.0e-12  /* EPA orientation, origin-on-face (:905, :910, :935) */
 #define TOL_POS  1.0e-15  /* IS_INSIDE_PF "positive" (:1306) */
 #define HULL_EPS 1.0e-10  /* re-supplied QuickHull: visibility / coplanarity threshold */
+#else
+/* Diagnostic build (oracle/Makefile: libgjkepa_oracle_f32.so): the same restatement in fp32
+ * arithmetic with the kernels' fp32 tolerances (csrc/gk_common.h Tol<float>), to study the fp32
+ * compute path on the CPU.  Every `double` below this point is a float; records stay fp64 structs. */
+#define TOL_PT   1.0e-6f
+#define TOL_Z    1.0e-12f
+#define TOL_ZO   1.0e-6f
+#define TOL_POS  1.0e-15f
+#define HULL_EPS 2.0e-6f
+#define double float
+#endif
+typedef double oreal;     /* the narrow phase's arithmetic type (float in the ORC_F32 build) */
 #define INIT_MAXIT 99     /* :86 */
 #define GJK_MAXIT  50     /* :186 */
 #define EPA_MAXIT  99     /* :299 */
@@ -332,6 +346,15 @@ static int cmp_dbl(const void* a, const void* b) {
     return (x > y) - (x < y);
 }
 
+/* diagnostic: nonzero -> epa() prints one line per iteration to stderr (single-threaded use only) */
+int oracle_epa_trace = 0;
+/* fp32 certificate thresholds (ORC_F32 only; see gjkepa_kernel.hip "fp32 certificate"): the largest
+ * drop of the polytope's MINLOC distance between iterations, and the largest support gap
+ * h_M(n) - depth at termination, both relative to max(1, depth). */
+double oracle_cert_drop = 1e-5, oracle_cert_gap = 1e-5;
+static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap */
+#include <stdio.h>
+
 /* EPA_solu loop (:274-323) with update_expandingPolytope_EPA (:863-1022). */
 static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
                double* depth, v3* normal, int* iters) {
@@ -367,7 +390,7 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
         }
         minv = H->d1[ml];
         double dt = dot(vsub(a1, ORIGIN), dir);
-        if (fabs(dt) < TOL_Z) {                                                    /* :905-908 */
+        if (fabs(dt) < TOL_ZO) {                                                   /* :905-908 */
             COV(ORC_BR_EPA_CENTROID);
             double sx = 0.0, sy = 0.0, sz = 0.0;
             for (int j = 0; j < 3; ++j)
@@ -379,9 +402,9 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
             M = mk(sx / cnt, sy / cnt, sz / cnt);
             dt = dot(vsub(a1, M), dir);
         }
-        if (dt <= -TOL_Z) { dir = vneg(dir); COV(ORC_BR_EPA_FLIP); }                /* :910 */
+        if (dt <= -TOL_ZO) { dir = vneg(dir); COV(ORC_BR_EPA_FLIP); }               /* :910 */
         v3 sp = support(A, B, dir);                                                  /* :914 */
-        int two = fabs(minv) < TOL_Z;                                                /* :935 */
+        int two = fabs(minv) < TOL_ZO;                                               /* :935 */
         if (two) COV(ORC_BR_EPA_TWO);
         /* --- hull of (polytope vertices + new point(s)) (:918-950) --- */
         if (iter == 1) {
@@ -425,6 +448,15 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
         } else {
             stop = F1 > F2;
             if (stop) COV(ORC_BR_EPA_STOP_SHRINK);
+        }
+        if (oracle_epa_trace)
+            fprintf(stderr, "it %2d F1 %3d F2 %3d minv %.9g dir (%.7g %.7g %.7g) sp (%.7g %.7g %.7g) h %.9g minv2 %.9g stop %d\n",
+                    iter, F1, F2, (double)minv, (double)dir.x, (double)dir.y, (double)dir.z, (double)sp.x,
+                    (double)sp.y, (double)sp.z, (double)dot(sp, dir), (double)minv2, stop);
+        {
+            double sc = minv > 1.0 ? minv : 1.0;
+            if (minv2 < minv - oracle_cert_drop * sc) g_cert |= 1;
+            if (stop && dot(sp, dir) - minv2 > oracle_cert_gap * sc) g_cert |= 2;
         }
         if (stop) { *depth = minv2; *normal = dir2; return 0; }
     }
@@ -709,7 +741,11 @@ do_epa:
         double depth = 0.0;
         v3 n = ORIGIN, pt = ORIGIN, q1, q2;
         int eit = 0;
+        g_cert = 0;
         st = epa(A, B, S, H, &depth, &n, &eit);
+#ifdef ORC_F32
+        out->reserved = (int8_t)(g_cert | (st ? 4 : 0));   /* diagnostic build: certificate flags */
+#endif
         out->diag = (uint32_t)(gjk_it & 0xff) | ((uint32_t)(eit & 0xff) << 8) |
                     ((uint32_t)(H->nf & 0xffff) << 16);
         if (st) goto fail;
@@ -742,14 +778,28 @@ fail: {
 }
 
 /* ---- public oracle entries ------------------------------------------------------------------ */
+#ifdef ORC_F32
+#undef double
+#endif
 int oracle_gjkepa(int32_t version, double tol_ff,
                   const double* p1, int32_t n1, const double* p2, int32_t n2,
                   gjkepa_contact_f64* out) {
     if (!out || (!p1 && n1 > 0) || (!p2 && n2 > 0)) return GJKEPA_E_ARG;
     hullbuf* H = (hullbuf*)malloc(sizeof(hullbuf));
     if (!H) return GJKEPA_E_ARG;
+#ifdef ORC_F32
+    oreal* c1 = (oreal*)malloc(sizeof(oreal) * (3 * (size_t)n1 + 1));
+    oreal* c2 = (oreal*)malloc(sizeof(oreal) * (3 * (size_t)n2 + 1));
+    for (int i = 0; i < 3 * n1; ++i) c1[i] = (oreal)p1[i];
+    for (int i = 0; i < 3 * n2; ++i) c2[i] = (oreal)p2[i];
+    hull_t A = {c1, n1}, B = {c2, n2};
+#else
     hull_t A = {p1, n1}, B = {p2, n2};
-    gjkepa_pair(version, tol_ff, &A, &B, H, out);
+#endif
+    gjkepa_pair(version, (oreal)tol_ff, &A, &B, H, out);
+#ifdef ORC_F32
+    free(c1); free(c2);
+#endif
     free(H);
     return 0;
 }
@@ -781,8 +831,8 @@ int oracle_gjkepa_batch_cov(int32_t version, double tol_ff, int32_t vert_dtype,
 #pragma omp parallel num_threads(nt)
     {
         hullbuf* H = (hullbuf*)malloc(sizeof(hullbuf));
-        double* b1 = (double*)malloc(sizeof(double) * 3 * GJKEPA_MAX_HULL_VERTS);
-        double* b2 = (double*)malloc(sizeof(double) * 3 * GJKEPA_MAX_HULL_VERTS);
+        oreal* b1 = (oreal*)malloc(sizeof(oreal) * 3 * GJKEPA_MAX_HULL_VERTS);
+        oreal* b2 = (oreal*)malloc(sizeof(oreal) * 3 * GJKEPA_MAX_HULL_VERTS);
 #pragma omp for schedule(dynamic, 64)
         for (int64_t k = 0; k < n_pairs; ++k) {
             int32_t ha = pairs[2 * k], hb = pairs[2 * k + 1];
@@ -794,21 +844,28 @@ int oracle_gjkepa_batch_cov(int32_t version, double tol_ff, int32_t vert_dtype,
                 if (cov) cov[k] = 1ull << ORC_BR_BAD_INPUT;
                 continue;
             }
-            if (vert_dtype == GJKEPA_DTYPE_F64) {
-                A.p = (const double*)verts + hull_off[ha];
-                B.p = (const double*)verts + hull_off[hb];
+            if (vert_dtype == GJKEPA_DTYPE_F64 && sizeof(oreal) == sizeof(double)) {
+                A.p = (const oreal*)verts + hull_off[ha];
+                B.p = (const oreal*)verts + hull_off[hb];
+            } else if (vert_dtype == GJKEPA_DTYPE_F64) {
+                const double* fa = (const double*)verts + hull_off[ha];
+                const double* fb = (const double*)verts + hull_off[hb];
+                for (int i = 0; i < 3 * na; ++i) b1[i] = (oreal)fa[i];
+                for (int i = 0; i < 3 * nb; ++i) b2[i] = (oreal)fb[i];
+                A.p = b1;
+                B.p = b2;
             } else {
                 const float* fa = (const float*)verts + hull_off[ha];
                 const float* fb = (const float*)verts + hull_off[hb];
-                for (int i = 0; i < 3 * na; ++i) b1[i] = (double)fa[i];
-                for (int i = 0; i < 3 * nb; ++i) b2[i] = (double)fb[i];
+                for (int i = 0; i < 3 * na; ++i) b1[i] = (oreal)fa[i];
+                for (int i = 0; i < 3 * nb; ++i) b2[i] = (oreal)fb[i];
                 A.p = b1;
                 B.p = b2;
             }
             A.n = na;
             B.n = nb;
             g_cov = 0;
-            gjkepa_pair(version, tol_ff, &A, &B, H, &out[k]);
+            gjkepa_pair(version, (oreal)tol_ff, &A, &B, H, &out[k]);
             if (cov) cov[k] = g_cov;
         }
         free(H); free(b1); free(b2);

@@ -70,6 +70,36 @@ def gjkepa_batch(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0)
     return out
 
 
+_lib32 = None
+
+
+def gjkepa_batch_f32(pool, version: int = 2, tol_ff: float = 1.0, nthreads: int = 0) -> np.ndarray:
+    """DIAGNOSTIC: the same restatement compiled in fp32 arithmetic with the kernels' fp32 tolerances
+    (gjkepa_oracle.c ORC_F32), to study the fp32-compute path on the CPU.  REC64 records holding fp32
+    values.  Not a parity reference for anything."""
+    global _lib32
+    if _lib32 is None:
+        p = os.path.join(_HERE, "build", "libgjkepa_oracle_f32.so")
+        if not os.path.exists(p):
+            build()
+        lib = ctypes.CDLL(p)
+        lib.oracle_gjkepa_batch.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                            ctypes.c_void_p, ctypes.c_int32]
+        lib.oracle_gjkepa_batch.restype = ctypes.c_int
+        _lib32 = lib
+    verts = np.ascontiguousarray(pool.verts, np.float32)
+    off = np.ascontiguousarray(pool.hull_off, np.int64)
+    cnt = np.ascontiguousarray(pool.hull_cnt, np.int32)
+    prs = np.ascontiguousarray(pool.pairs, np.int32).reshape(-1)
+    n = prs.size // 2
+    out = np.zeros(n, REC64)
+    rc = _lib32.oracle_gjkepa_batch(int(version), float(tol_ff), 0, verts.ctypes.data, off.ctypes.data,
+                                    cnt.ctypes.data, prs.ctypes.data, n, out.ctypes.data, int(nthreads))
+    assert rc == 0
+    return out
+
+
 # ORC_BR_* bit names (gjkepa_oracle.h), in bit order
 BRANCHES = [
     "SPHERE_MISS", "INIT_RETRY", "INIT_CAP", "INIT_S3_COINCIDE", "INIT_TRI_HIT", "INIT_TRI_PLANE",

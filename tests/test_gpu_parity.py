@@ -156,29 +156,26 @@ def test_device_api_matches_host_api():
     assert out.cpu().numpy().tobytes() == host.tobytes()
 
 
-def fp32_errors(g, r):
-    """Per-hit errors of fp32-compute records g against fp64 oracle records r (both OK hits):
-    relative depth error and the angle (rad) between the normals."""
-    m = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
-    dr = r["penetration_depth"][m].astype(np.float64)
-    de = np.abs(g["penetration_depth"][m].astype(np.float64) - dr) / np.maximum(np.abs(dr), 1e-9)
-    a = g["collision_normal"][m].astype(np.float64)
-    b = r["collision_normal"][m].astype(np.float64)
-    cosang = np.sum(a * b, axis=1) / np.maximum(np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1), 1e-300)
-    return de, np.arccos(np.clip(cosang, -1.0, 1.0))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_fp32_tolerance_sweep(orc):
-    """fp32 compute (throughput path): hit flags vs the fp64 oracle, and gates on the depth and
-    normal errors: p99.9 relative depth error < 1e-5 and p99.9 normal angle < 1e-5
-    rad; a pair whose fp32 polytope picks a different near-tied face can be off by more, so the
-    tail is bounded separately (depth 1e-3 relative, angle 0.05 rad)."""
-    for name, lo, hi, rmax in [("C2", 32, 32, 2.5), ("C5", 64, 128, 0.3)]:
-        pool = gjkepa.synth_pairs(0x6A4B5C1D, 4000, lo, hi, rmax)
-        g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F32)
-        r = orc.gjkepa_batch(pool, 2, 1.0)
-        agree = (g["collision"] == r["collision"]).mean()
-        assert agree >= 0.999, (name, agree)
-        de, ang = fp32_errors(g, r)
-        assert np.quantile(de, 0.999) < 1e-5 and de.max() < 1e-3, (name, np.quantile(de, 0.999), de.max())
-        assert np.quantile(ang, 0.999) < 1e-5 and ang.max() < 0.05, (name, np.quantile(ang, 0.999), ang.max())
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_fp32_tolerance_sweep(cfg):
+    """fp32 compute (throughput path) on the full 2^20-pair C2 / C5 batches against the
+    fp64 path (byte-identical to the oracle: test_gpu_fullsize, bench parity_sample): hit flags
+    identical; every pair fp64 answers as an OK hit is an OK hit in fp32; depth within 1e-3 relative
+    (+ 4e-6 absolute, the fp32 polytope's resolution); normal within 0.05 rad unless the fp32 normal
+    is itself a minimum-depth direction (a tie: its support gap on the Minkowski difference is within
+    1e-6 of the depth).  Uncertified fp32 answers are recomputed in fp64 by the chain itself
+    (gjkepa_kernel.hip "fp32 certificate"); before that, C5 had a pair 20% off in depth."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from bench import CONFIGS, SEED
+    from fp32_metrics import fp32_report, passes
+    nmin, nmax, rmax, n, _ = CONFIGS[cfg]
+    pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax)
+    g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F32)
+    r = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F64)
+    rep = fp32_report(pool, g, r)
+    assert passes(rep), (cfg, rep)
+    assert rep["depth_relerr_p999"] < 1e-5 and rep["normal_angle_rad_p999"] < 1e-5, (cfg, rep)
