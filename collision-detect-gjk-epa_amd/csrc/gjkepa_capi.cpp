@@ -40,7 +40,13 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(GJKEPA_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-constexpr int64_t kWsHeader = 256;
+constexpr int64_t kWsHeader = 512;      // counters, tallies, park slot counter (gjkepa_workspace_bytes)
+constexpr int kWsParkWord = GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY;
+// Workspace = header | one route byte per pair | park slots (GJKEPA_PARK_BYTES each, from the first
+// 256-byte boundary after the route bytes).  gjkepa_workspace_bytes sizes the park area for one pair in
+// kParkShare (C4 parks 9.2% of its pairs); whatever a caller provides beyond the route bytes is used.
+constexpr int64_t kParkShare = 8;
+int64_t ws_base(int64_t n) { return (kWsHeader + n + 255) / 256 * 256; }
 constexpr int kSparseClaim = 16;
 #ifndef GJKEPA_OVERLAP_MIN
 #define GJKEPA_OVERLAP_MIN (1 << 16)
@@ -240,11 +246,13 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
             void* out, void* workspace, int64_t ws_bytes, hipStream_t s, int num_cus, uint32_t* warm = nullptr) {
     if (n_pairs == 0) return 0;
-    if (ws_bytes < gjkepa_workspace_bytes(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
+    // the header and the route bytes are required; park slots are used as far as the caller provides them
+    if (ws_bytes < ws_base(n_pairs)) return fail(GJKEPA_E_WORKSPACE, "workspace too small");
     // workspace: per-launch chunk counters and route tallies (zeroed here), then one route byte per
     // pair (written by GJK tier 0 for every pair before any read)
     uint32_t* ctr = (uint32_t*)workspace;
     uint8_t* route = (uint8_t*)workspace + kWsHeader;
+    const int64_t park_slots = ws_bytes > ws_base(n_pairs) ? (ws_bytes - ws_base(n_pairs)) / GJKEPA_PARK_BYTES : 0;
     hipError_t e;
     if (!warm && n_pairs <= kFusedMax) {                 // small batch: one launch, one wave per pair
         gjkepa_epa_args q{};
@@ -261,10 +269,10 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         if ((e = gjkepa_launch_query(vert_dtype, precision, q, s)) != hipSuccess) return hip_fail(e, "query kernel launch");
         return 0;
     }
-    static_assert(sizeof(uint32_t) * (GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY) <= kWsHeader, "workspace header");
-    // counter / tally reset: a one-wave kernel rather than a memset, so a captured chain is kernel
-    // nodes only
-    if ((e = gjkepa_launch_ws_reset(ctr, GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY, s)) != hipSuccess)
+    static_assert(sizeof(uint32_t) * (kWsParkWord + 1) <= kWsHeader, "workspace header");
+    // counter / tally / park counter reset: a one-wave kernel rather than a memset, so a captured
+    // chain is kernel nodes only
+    if ((e = gjkepa_launch_ws_reset(ctr, kWsParkWord + 1, s)) != hipSuccess)
         return hip_fail(e, "workspace counter reset");
     uint32_t* tally = ctr + GJKEPA_WS_COUNTERS;
     int launch = 0;
@@ -301,6 +309,9 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     a.tally = tally;
     a.out = out;
     a.num_cus = num_cus;
+    a.park = park_slots > 0 ? (unsigned char*)workspace + ws_base(n_pairs) : nullptr;
+    a.park_ctr = ctr + kWsParkWord;
+    a.park_cap = (uint32_t)(park_slots < (int64_t)UINT32_MAX ? park_slots : UINT32_MAX);
     // small batches (e.g. combined single-pair queries) keep one stream: the fork's events and extra
     // launches cost more latency than the overlap saves
     Fork* f = nullptr;
@@ -412,7 +423,7 @@ int gjkepa_record_bytes(int32_t precision) {
 
 int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
     if (n_pairs < 0) return GJKEPA_E_ARG;
-    return kWsHeader + n_pairs;
+    return ws_base(n_pairs) + (n_pairs + kParkShare - 1) / kParkShare * GJKEPA_PARK_BYTES;
 }
 
 const char* gjkepa_last_error(void) { return g_err.c_str(); }

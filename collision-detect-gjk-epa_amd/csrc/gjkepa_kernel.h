@@ -249,6 +249,21 @@
 // the end of the chain (gjkepa_kernel.hip "fp32 certificate")
 #define GJKEPA_ROUTE_REDO 0x2E
 
+// Polytope parking.  EPA tiers 2 and 3 hand a pair whose polytope is about to outgrow them to tier 4
+// with its polytope instead of its GJK simplex: the state at the start of an iteration (vertices,
+// face slots with their vertex ids and creation keys, counters, the MINLOC direction) goes to a park
+// slot in the workspace and tier 4 resumes from it, recomputing each face's plane from its vertices
+// (the same arithmetic, so the same bits).  Results are those of a restart: the keys carry the face
+// order, and a polytope does not depend on where its faces sit.  When the park slots run out a pair
+// restarts from the simplex as before.
+#ifndef GJKEPA_PARK
+#define GJKEPA_PARK 1                 // 0: restart from the simplex (A/B)
+#endif
+#define GJKEPA_PARK_VC 72             // largest polytope parked: tier 2's (tier 3's is 40 / 64)
+#define GJKEPA_PARK_FC 128
+#define GJKEPA_PARK_HDR 128           // header: counters (64 B) and direction / distances (<= 64 B)
+#define GJKEPA_PARK_BYTES (GJKEPA_PARK_HDR + 3 * 8 * GJKEPA_PARK_VC + 2 * 4 * GJKEPA_PARK_FC)   // 2880
+
 // gjkepa_*_args::grid: > 0 explicit, 0 occupancy x CUs (looping workgroups), GJKEPA_GRID_UNITS one
 // workgroup per work unit
 #define GJKEPA_GRID_UNITS (-2)
@@ -289,6 +304,9 @@ struct gjkepa_epa_args {
     void* out;
     int grid;
     int num_cus;
+    unsigned char* park;        // park slots (GJKEPA_PARK_BYTES each), nullptr: none
+    uint32_t* park_ctr;         // park slots taken so far (workspace header)
+    uint32_t park_cap;          // park slots available
     uint32_t guard;             // gjkepa_guard_of(*this): checked at kernel entry in GJKEPA_DIAG_GUARD builds
 };
 
@@ -319,6 +337,7 @@ __host__ __device__ inline uint32_t gjkepa_guard_of(const gjkepa_epa_args& a) {
     h = gjkepa_mix(h, (uint64_t)(int64_t)a.ct_base); h = gjkepa_mix(h, (uint64_t)a.ctr);
     h = gjkepa_mix(h, (uint64_t)(int64_t)a.claim); h = gjkepa_mix(h, (uint64_t)a.tally); h = gjkepa_mix(h, (uint64_t)a.out);
     h = gjkepa_mix(h, (uint64_t)(int64_t)a.grid); h = gjkepa_mix(h, (uint64_t)(int64_t)a.num_cus);
+    h = gjkepa_mix(h, (uint64_t)a.park); h = gjkepa_mix(h, (uint64_t)a.park_ctr); h = gjkepa_mix(h, (uint64_t)a.park_cap);
     return gjkepa_fold(h);
 }
 

@@ -34,6 +34,7 @@ namespace gk {
 
 constexpr int ST_DEFER = 100;   // internal: does not fit this tier
 constexpr int ST_REDO = 103;    // internal (fp32 compute): answer not certified, recompute in fp64
+constexpr int ST_PARKED = 104;  // internal: polytope parked for the next tier (gjkepa_kernel.h "Polytope parking")
 
 // fp32 certificate.  An fp32 EPA can build an invalid polytope from inconsistent visibility decisions
 // on near-coplanar faces (the fp32 rounding of a sliver's normal), after which its MINLOC distance
@@ -1049,13 +1050,124 @@ CTX_T DEV int epa_step(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     return epa_grow(c, S, false);
 }
 
-CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf) {
+// ---- polytope parking (gjkepa_kernel.h): park slot layout
+//   u32 [0..15]   nv, hw, nf, F1, iters, kbase, neg, av, gjk_it
+//   T   @64       dir.x, dir.y, dir.z, minv, hsup
+//   T   @HDR      vx[PARK_VC], vy[PARK_VC], vz[PARK_VC]      (vertex coordinates by id)
+//   u32 @HDR+3*8*PARK_VC   fv[PARK_FC], key[PARK_FC]        (face slots below hw; kEmpty = hole)
+struct ParkCtl {
+    unsigned char* base;     // park slots
+    uint32_t* ctr;           // slots taken
+    uint32_t cap;            // slots available
+    uint32_t gjk_it;         // GJK iterations of the pair (kept in the parked state)
+    uint32_t* slot;          // the pair's record slot: word 5 <- park slot + 1
+};
+constexpr int kParkFaces = GJKEPA_PARK_HDR + 3 * 8 * GJKEPA_PARK_VC;
+
+// At the start of an iteration: park the polytope when the next iteration could outgrow this tier
+// (two insertions add at most two vertices and four faces to a valid polytope), if a slot is free.
+CTX_T DEV bool park_now(CTX& c, const EPAST_T& S, const ParkCtl& pk) {
+    static_assert(VC <= GJKEPA_PARK_VC && FC <= GJKEPA_PARK_FC, "parked polytope larger than a park slot");
+    constexpr int R = (FC + G - 1) / G;
+    if (!c.g.unib(S.nv + 2 > VC || S.nf + 4 > FC)) return false;
+    const int gl = c.g.gl;
+    uint32_t idx = 0;
+    if (gl == 0) idx = atomicAdd(pk.ctr, 1u);
+    idx = (uint32_t)__shfl((int)idx, c.g.lane & ~(G - 1));
+    if (c.g.unib(idx >= pk.cap)) return false;                 // slots used up: run on, restart later
+    unsigned char* rec = pk.base + (size_t)idx * GJKEPA_PARK_BYTES;
+    auto& E = c.L.u.e;
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(rec);
+    T* tv = reinterpret_cast<T*>(rec + 64);
+    T* vx = reinterpret_cast<T*>(rec + GJKEPA_PARK_HDR);
+    uint32_t* fv = reinterpret_cast<uint32_t*>(rec + kParkFaces);
+    if (gl < 9) {
+        const uint32_t h[9] = {(uint32_t)S.nv, (uint32_t)S.hw, (uint32_t)S.nf, (uint32_t)S.F1, (uint32_t)S.iters, S.kbase,
+                               (uint32_t)S.neg, (uint32_t)S.av, pk.gjk_it};
+        uint32_t w = h[0];
+#pragma unroll
+        for (int j = 1; j < 9; ++j) w = gl == j ? h[j] : w;
+        hdr[gl] = w;
+    }
+    if (gl < 5) {
+        const T hs = certify<T>() ? S.hsup : T(0);
+        tv[gl] = gl == 0 ? S.dir.x : gl == 1 ? S.dir.y : gl == 2 ? S.dir.z : gl == 3 ? S.minv : hs;
+    }
+    for (int i = gl; i < S.nv; i += G) {
+        vx[i] = E.vx[i];
+        vx[GJKEPA_PARK_VC + i] = E.vy[i];
+        vx[2 * GJKEPA_PARK_VC + i] = E.vz[i];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        if (f < S.hw) { fv[f] = S.F.fv[r]; fv[GJKEPA_PARK_FC + f] = S.F.key[r]; }
+    }
+    if (gl == 0) pk.slot[5] = idx + 1;
+    return true;
+}
+
+// Resume a parked polytope (the next tier's first step is epa_grow): vertices back into LDS, each
+// face's plane recomputed from its vertex ids exactly as it was built (UNINML of the stored order,
+// DIST_PF_SIGN from its first vertex), slot f in slot f (holes stay holes).
+CTX_T DEV void epa_resume(CTX& c, EPAST_T& S, const unsigned char* rec, uint32_t& gjk_it) {
+    constexpr int R = (FC + G - 1) / G;
+    auto& E = c.L.u.e;
+    const int gl = c.g.gl;
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(rec);
+    const T* tv = reinterpret_cast<const T*>(rec + 64);
+    const T* vx = reinterpret_cast<const T*>(rec + GJKEPA_PARK_HDR);
+    const uint32_t* fv = reinterpret_cast<const uint32_t*>(rec + kParkFaces);
+    S.nv = c.g.uni((int)hdr[0]); S.hw = c.g.uni((int)hdr[1]); S.nf = c.g.uni((int)hdr[2]); S.F1 = c.g.uni((int)hdr[3]);
+    S.iters = c.g.uni((int)hdr[4]); S.kbase = hdr[5]; S.neg = hdr[6] != 0; S.av = (int)hdr[7]; gjk_it = hdr[8];
+    S.dir = vmk<T>(tv[0], tv[1], tv[2]);
+    S.minv = tv[3];
+    S.hsup = tv[4];
+    S.unchanged = false;
+    for (int i = gl; i < S.nv; i += G) {
+        E.vx[i] = vx[i];
+        E.vy[i] = vx[GJKEPA_PARK_VC + i];
+        E.vz[i] = vx[2 * GJKEPA_PARK_VC + i];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        S.F.fv[r] = kEmpty;
+        if (f < S.hw) {
+            const uint32_t w = fv[f];
+            if (!(w & kEmpty)) {
+                const V3<T> U = c.vert((int)(w & 0xffu)), W = c.vert((int)((w >> 8) & 0xffu)), P = c.vert((int)((w >> 16) & 0xffu));
+                const V3<T> n = uninml(U, W, P);
+                S.F.nx[r] = n.x; S.F.ny[r] = n.y; S.F.nz[r] = n.z;
+                S.F.d[r] = dot(vsub(zero3<T>(), U), n);
+                S.F.fv[r] = w;
+                S.F.key[r] = fv[GJKEPA_PARK_FC + f];
+            }
+        }
+    }
+}
+
+// EPA from the simplex (or, with `rec`, from a parked polytope); with `pk`, the polytope is parked
+// (ST_PARKED) when it could outgrow this tier and a park slot is free.
+CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf,
+                  const ParkCtl* pk = nullptr, const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
     EPAST_T S;
-    int st = epa_begin(c, S, s0, s1, s2, s3);
-    while (st == 0) {
-        st = epa_step(c, S, depth, normal);
-        if (st == ST_CONT) st = 0;
-        else break;
+    int st;
+    if (rec) {
+        epa_resume(c, S, rec, *gjk_it);
+        st = epa_grow(c, S, false);
+    } else {
+        st = epa_begin(c, S, s0, s1, s2, s3);     // iteration 1 up to its hull; it closes in the loop
+        if (st == 0) st = ST_CONT;
+    }
+    while (st == ST_CONT) {
+        st = epa_close(c, S, depth, normal);
+        if (st != ST_CONT) break;
+        if constexpr (VC <= GJKEPA_PARK_VC && FC <= GJKEPA_PARK_FC) {
+            if (pk && park_now(c, S, *pk)) { st = ST_PARKED; break; }
+        }
+        st = epa_grow(c, S, false);
     }
     iters = S.iters;
     nf = S.nf;
@@ -1636,12 +1748,14 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 
 // EPA_solu's polytope loop (:274-323) from the GJK simplex: 0 (depth, n filled), an error
 // status or ST_DEFER; `diag_epa` gets (epa_iters << 8) | (faces << 16).
-CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t& diag_epa) {
-    const V3<T> s0 = decode_pt(c, kc[0]), s1 = decode_pt(c, kc[1]), s2 = decode_pt(c, kc[2]), s3 = decode_pt(c, kc[3]);
+CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t& diag_epa, const ParkCtl* pk = nullptr,
+                        const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
+    V3<T> s0 = zero3<T>(), s1 = s0, s2 = s0, s3 = s0;
+    if (!rec) { s0 = decode_pt(c, kc[0]); s1 = decode_pt(c, kc[1]); s2 = decode_pt(c, kc[2]); s3 = decode_pt(c, kc[3]); }
     depth = 0;
     n = zero3<T>();
     int eit = 0, nf = 0;
-    const int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf);
+    const int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf, pk, rec, gjk_it);
     diag_epa = ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
     return st;
 }
@@ -1993,10 +2107,10 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
                                           : (r == PH_MISS && gl == 0) ? kWarmMiss : kStale;
                 if (r == PH_HIT) {
 #pragma unroll
-                    for (int j0 = 0; j0 < 5; j0 += G) {
+                    for (int j0 = 0; j0 < 6; j0 += G) {   // simplex codes, GJK iterations, no parked polytope
                         const int j = j0 + gl;
-                        const uint32_t word = j == 0 ? kc[0] : j == 1 ? kc[1] : j == 2 ? kc[2] : j == 3 ? kc[3] : (uint32_t)gjk_it;
-                        if (j < 5) reinterpret_cast<uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + j] = word;
+                        const uint32_t word = j == 0 ? kc[0] : j == 1 ? kc[1] : j == 2 ? kc[2] : j == 3 ? kc[3] : j == 4 ? (uint32_t)gjk_it : 0u;
+                        if (j < 6) reinterpret_cast<uint32_t*>(a.out)[pair * (sizeof(T) == 8 ? 32 : 16) + j] = word;
                     }
                     next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(na > nb ? na : nb));
                 } else if (r == PH_MISS) {
@@ -2031,7 +2145,8 @@ DEV int contact_tier_for(int nmax) { return nmax <= GJKEPA_C0_G * GJKEPA_C0_K ? 
 // EPA kernel: the polytope loop for the pairs routed to this tier.  Depth, normal and the
 // diagnostics are parked in their final record fields and the pair goes to its contact tier.  A
 // polytope that outgrows the tier is routed to the next one (recomputed from the simplex codes).
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH>
+// PR bit 0: park a polytope about to outgrow this tier (tier 3); bit 1: resume parked ones (tier 4).
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int PR>
 __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, VC, FC>;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -2063,12 +2178,18 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
         const int r = GJKEPA_STATUS_DEGENERATE;
         depth = 0; n = zero3<T>();
 #else
-        const int r = (c.na > G * K || c.nb > G * K) ? ST_DEFER : epa_phase(c, kc, depth, n, de);
+        const uint32_t parked = (PR & 2) && a.park ? slot[5] : 0u;   // park slot + 1 (tiers 2, 3)
+        uint32_t it_park = gjk_it;
+        const ParkCtl pk{a.park, a.park_ctr, a.park_cap, gjk_it, slot};
+        const bool can_park = (PR & 1) && a.park && a.next_code >= 0;
+        const int r = (c.na > G * K || c.nb > G * K) ? ST_DEFER
+                    : epa_phase(c, kc, depth, n, de, can_park ? &pk : nullptr,
+                                parked ? a.park + (size_t)(parked - 1) * GJKEPA_PARK_BYTES : nullptr, &it_park);
 #endif
         __builtin_amdgcn_wave_barrier();
         const uint32_t diag = (gjk_it & 0xffu) | de;
         uint8_t next = 0;
-        if (r == ST_DEFER && a.next_code >= 0) {   // next tier that holds the hulls
+        if ((r == ST_DEFER || r == ST_PARKED) && a.next_code >= 0) {   // next tier that holds the hulls
             next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
         } else if (redo_status<T>(r, a.next_code < 0)) {   // fp32: not certified, recomputed in fp64
             next = GJKEPA_ROUTE_REDO;
@@ -2137,8 +2258,9 @@ struct PairQueue {
 // EPA tier kernel with group refill: a group whose pair finished takes the next pair between
 // two EPA iterations (once at least REFILL groups of the wave are idle), so a wave no longer
 // runs every round to its slowest pair.  Results are the same as epa_kernel's.
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL, int PR>
 __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_args a) {
+    static_assert(!(PR & 2), "refill tiers do not resume parked polytopes");
     constexpr int R = (FC + G - 1) / G;
     constexpr int NG = 64 / G;
     using L_t = Lds<T, TIn, G, K, VC, FC>;
@@ -2164,7 +2286,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
         uint32_t* slot = reinterpret_cast<uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16);
         const uint32_t diag = (gjk_it & 0xffu) | ((uint32_t)(S.iters & 0xff) << 8) | ((uint32_t)(S.nf & 0xffff) << 16);
         uint8_t next = 0;
-        if (r == ST_DEFER && a.next_code >= 0) {
+        if ((r == ST_DEFER || r == ST_PARKED) && a.next_code >= 0) {
             next = (uint8_t)(GJKEPA_ROUTE_EPA0 + epa_tier_for(c.na > c.nb ? c.na : c.nb, a.next_code - GJKEPA_ROUTE_EPA0, VC));
         } else if (redo_status<T>(r, a.next_code < 0)) {   // fp32: not certified, recomputed in fp64
             next = GJKEPA_ROUTE_REDO;
@@ -2230,6 +2352,13 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
             V3<T> n = zero3<T>();
             int r = ST_CONT;
             if (!seeded) r = epa_close(c, S, depth, n);
+            if constexpr ((PR & 1) != 0) {                 // park a polytope about to outgrow this tier
+                if (r == ST_CONT && !seeded && a.park && a.next_code >= 0) {
+                    const ParkCtl pk{a.park, a.park_ctr, a.park_cap, gjk_it,
+                                     reinterpret_cast<uint32_t*>(a.out) + pair * (sizeof(T) == 8 ? 32 : 16)};
+                    if (park_now(c, S, pk)) r = ST_PARKED;
+                }
+            }
             if (r == ST_CONT) r = epa_grow(c, S, seeded);
             seeded = false;
             __builtin_amdgcn_wave_barrier();
@@ -2556,11 +2685,11 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL = 0>
+template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL = 0, int PR = 0>
 hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
     auto kfn = [] {
-        if constexpr (REFILL > 0) return gk::epa_kernel_refill<TIn, T, G, K, VC, FC, MINW, LH, REFILL>;
-        else return gk::epa_kernel<TIn, T, G, K, VC, FC, MINW, LH>;
+        if constexpr (REFILL > 0) return gk::epa_kernel_refill<TIn, T, G, K, VC, FC, MINW, LH, REFILL, PR>;
+        else return gk::epa_kernel<TIn, T, G, K, VC, FC, MINW, LH, PR>;
     }();
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, VC, FC>, G>() * GPW;
@@ -2603,9 +2732,9 @@ hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     switch (tier) {
         case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
         case 1: return launch_epa<TIn, T, EPA_ARGS(1), GJKEPA_E1_REFILL>(a, s);
-        case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL>(a, s);
-        case 3: return launch_epa<TIn, T, EPA_ARGS(3)>(a, s);
-        case 4: return launch_epa<TIn, T, EPA_ARGS(4)>(a, s);
+        case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL, GJKEPA_PARK ? 1 : 0>(a, s);   // parks
+        case 3: return launch_epa<TIn, T, EPA_ARGS(3), 0, GJKEPA_PARK ? 1 : 0>(a, s);                  // parks
+        case 4: return launch_epa<TIn, T, EPA_ARGS(4), 0, GJKEPA_PARK ? 2 : 0>(a, s);                  // resumes
         default: return launch_epa<TIn, T, EPA_ARGS(5)>(a, s);
     }
 }

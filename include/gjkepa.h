@@ -148,10 +148,14 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
                  void* out, int32_t device);
 
 /* ---- batch over device buffers (asynchronous on `stream`, a hipStream_t or NULL) -------------
- * All pointers are device pointers on the current device.  `workspace` (4-byte aligned) must hold
- * at least gjkepa_workspace_bytes(n_pairs) bytes: a 256-byte header of per-kernel work counters
- * (reset by the call itself) and one routing byte per pair (which GJK / EPA / contact kernel tier
- * owns the pair next).  It may be reused between calls on the same stream. */
+ * All pointers are device pointers on the current device.  `workspace` (256-byte aligned) should hold
+ * gjkepa_workspace_bytes(n_pairs) bytes: a 512-byte header of per-kernel work counters and route
+ * tallies (reset by the call itself), one routing byte per pair (which GJK / EPA / contact kernel
+ * tier owns the pair next), and park slots of 2880 bytes for one pair in 8: an EPA tier whose
+ * polytope is about to outgrow it parks the polytope there and the next tier resumes it instead of
+ * restarting from the GJK simplex (results identical either way).  The minimum is the header plus
+ * the route bytes rounded up to 256; park slots are used as far as the workspace provides them.  It
+ * may be reused between calls on the same stream. */
 int64_t gjkepa_workspace_bytes(int64_t n_pairs);
 int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
                         const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
