@@ -263,7 +263,10 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
         m = fmaxf(m, sv[k]);
     }
     m = gmax<G>(m);
-    const float thr = m - 0x1p-18f * ((fabsf(fx) + fabsf(fy) + fabsf(fz)) * vmax);
+    // a bound below 2^-90 may have lost terms to fp32 underflow (|d_i| |v| flushed): then every vertex
+    // is a candidate (the plain fp64 scan), as for a non-finite screen
+    const float bnd = (fabsf(fx) + fabsf(fy) + fabsf(fz)) * vmax;
+    const float thr = bnd >= 0x1p-90f ? m - 0x1p-18f * bnd : -INFINITY;
     uint32_t cand = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -999,8 +1002,20 @@ CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     if (S.F1 == F2) stop = S.unchanged || sorted_equal(c, S.F, S.hw);   // unchanged hull: identical sorted lists
     else stop = S.F1 > F2;
     GK_STAMP(SE_TERM);
-    if constexpr (certify<T>()) {                             // fp32 certificate: closed support gap
-        if (stop && c.g.unib(S.hsup - S.minv > Tol<T>::CERT_GAP * (S.minv > T(1) ? S.minv : T(1)))) return ST_REDO;
+    if constexpr (certify<T>()) {
+        // fp32 certificate at termination: closed support gap; a depth above fp32 resolution; the
+        // origin strictly below every face (a hit the polytope itself proves)
+        if (stop) {
+            constexpr int R = (FC + G - 1) / G;
+            bool out = false;
+#pragma unroll
+            for (int r = 0; r < R; ++r) out = out || (!(S.F.fv[r] & kEmpty) && !(S.F.d[r] < T(0)));
+            const float sc = c.vmax_a + c.vmax_b;
+            if (c.g.any(out) ||
+                c.g.unib(S.hsup - S.minv > Tol<T>::CERT_GAP * (S.minv > T(1) ? S.minv : T(1)) ||
+                         !(S.minv > Tol<T>::CERT_TOUCH * (sc > 1.0f ? sc : 1.0f))))
+                return ST_REDO;
+        }
     }
     if (stop) { depth = S.minv; normal = dir2; return 0; }
     // ---- next iteration: same faces as this iteration's F2, so its MINLOC carries over
@@ -1796,7 +1811,8 @@ CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* 
 CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restrict__ pb) {
     const int gl = c.g.gl;
     bool nonfinite = false;
-    constexpr bool kScreen = ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4;
+    // the hulls' largest |coordinate|: the fp32 support screen's bound, the fp32 certificate's scale
+    constexpr bool kScreen = (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) || certify<T>();
     float ma = 0.0f, mb = 0.0f;     // largest |coordinate| (support screen bound; padding lanes hold 0)
 #pragma unroll
     for (int k = 0; k < K; ++k) {

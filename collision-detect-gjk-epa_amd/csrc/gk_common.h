@@ -38,6 +38,9 @@ template <> struct Tol<float> {              // fp32 throughput path: tolerances
     // between iterations, and largest support gap h_M(n) - depth at termination, relative to max(1, depth)
     static constexpr float CERT_DROP = 1.0e-5f;
     static constexpr float CERT_GAP = 1.0e-5f;
+    // and the smallest depth it answers itself, relative to max(1, |A| + |B|) (largest |coordinate| of
+    // each hull): a touching pair's hit flag and depth are below fp32 resolution
+    static constexpr float CERT_TOUCH = 1.0e-5f;
 };
 
 DEV double tsqrt(double x) { return ::sqrt(x); }

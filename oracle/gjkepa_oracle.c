@@ -351,8 +351,9 @@ int oracle_epa_trace = 0;
 /* fp32 certificate thresholds (ORC_F32 only; see gjkepa_kernel.hip "fp32 certificate"): the largest
  * drop of the polytope's MINLOC distance between iterations, and the largest support gap
  * h_M(n) - depth at termination, both relative to max(1, depth). */
-double oracle_cert_drop = 1e-5, oracle_cert_gap = 1e-5;
-static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap */
+double oracle_cert_drop = 1e-5, oracle_cert_gap = 1e-5, oracle_cert_touch = 1e-5;
+static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: touch / outside */
+static _Thread_local double g_cert_scale;   /* max |coordinate| of A + that of B */
 #include <stdio.h>
 
 /* EPA_solu loop (:274-323) with update_expandingPolytope_EPA (:863-1022). */
@@ -457,6 +458,12 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
             double sc = minv > 1.0 ? minv : 1.0;
             if (minv2 < minv - oracle_cert_drop * sc) g_cert |= 1;
             if (stop && dot(sp, dir) - minv2 > oracle_cert_gap * sc) g_cert |= 2;
+            if (stop) {
+                int out = 0;
+                for (int f = 0; f < F2; ++f) out |= !(H->f[f].sd < 0.0);
+                double ts = g_cert_scale > 1.0 ? g_cert_scale : 1.0;
+                if (out || !(minv2 > oracle_cert_touch * ts)) g_cert |= 8;
+            }
         }
         if (stop) { *depth = minv2; *normal = dir2; return 0; }
     }
@@ -742,6 +749,12 @@ do_epa:
         v3 n = ORIGIN, pt = ORIGIN, q1, q2;
         int eit = 0;
         g_cert = 0;
+        {
+            double ma = 0.0, mb = 0.0;
+            for (int i = 0; i < 3 * A->n; ++i) { double t = fabs(A->p[i]); if (t > ma) ma = t; }
+            for (int i = 0; i < 3 * B->n; ++i) { double t = fabs(B->p[i]); if (t > mb) mb = t; }
+            g_cert_scale = ma + mb;
+        }
         st = epa(A, B, S, H, &depth, &n, &eit);
 #ifdef ORC_F32
         out->reserved = (int8_t)(g_cert | (st ? 4 : 0));   /* diagnostic build: certificate flags */

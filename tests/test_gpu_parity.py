@@ -159,9 +159,9 @@ def test_device_api_matches_host_api():
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C5"])
+@pytest.mark.parametrize("cfg", ["C2", "C5", "C4"])
 def test_fp32_tolerance_sweep(cfg):
-    """fp32 compute (throughput path) on the full 2^20-pair C2 / C5 batches against the
+    """fp32 compute (throughput path) on the full C2 / C5 (2^20) and C4 (2^22) batches against the
     fp64 path (byte-identical to the oracle: test_gpu_fullsize, bench parity_sample): hit flags
     identical; every pair fp64 answers as an OK hit is an OK hit in fp32; depth within 1e-3 relative
     (+ 4e-6 absolute, the fp32 polytope's resolution); normal within 0.05 rad unless the fp32 normal

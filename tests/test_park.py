@@ -1,0 +1,65 @@
+"""Polytope parking (gjkepa_kernel.h "Polytope parking"): EPA tiers 2 and 3
+park a polytope about to outgrow them in the workspace's park slots and tier 4 resumes it instead of
+restarting from the GJK simplex (EPA_solu's loop, GCLIB_GJKEPA.f90:274-323, continued where it was).
+The records must not depend on it: with park slots, without any (the minimum workspace: every
+overflow restarts), and the oracle's, byte for byte, on pairs that do overflow (large hulls, deep
+overlaps: C4's 129-256-vertex tier, C5's 33-128-vertex tier)."""
+import numpy as np
+import pytest
+
+import gjkepa
+
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED0F
+
+
+def _run(pool, ws_bytes, precision=gjkepa.PREC_F64):
+    import torch
+    dev = torch.device("cuda", 0)
+    v = torch.from_numpy(pool.verts).to(dev)
+    o = torch.from_numpy(pool.hull_off).to(dev)
+    c = torch.from_numpy(pool.hull_cnt).to(dev)
+    p = torch.from_numpy(pool.pairs.reshape(-1).copy()).to(dev)
+    n = pool.n_pairs
+    out = torch.zeros(n * gjkepa.load().gjkepa_record_bytes(precision), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+    gjkepa.gjkepa_batch_device(2, 1.0, pool.dtype_code, precision, v.data_ptr(), o.data_ptr(), c.data_ptr(),
+                               p.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes, 0)
+    torch.cuda.synchronize()
+    parked = int(ws[64 * 4:65 * 4].cpu().numpy().view(np.uint32)[0])     # header word 64: park slots taken
+    return np.frombuffer(out.cpu().numpy().tobytes(), gjkepa.record_dtype(precision)), parked
+
+
+@pytest.mark.parametrize("lo,hi,rmax", [(129, 256, 0.6), (40, 128, 0.3)])
+def test_parked_polytopes_resume_bitexact(orc, lo, hi, rmax):
+    n = 6000
+    pool = gjkepa.synth_pairs(SEED, n, lo, hi, rmax)
+    full, parked = _run(pool, gjkepa.workspace_bytes(n))
+    minimum = (512 + n + 255) // 256 * 256                 # header + route bytes: no park slots
+    bare, parked0 = _run(pool, minimum)
+    assert parked0 == 0, parked0
+    assert parked > 20, f"expected overflowing polytopes to park, got {parked}"
+    assert full.tobytes() == bare.tobytes()
+    ref = orc.gjkepa_batch(pool, 2, 1.0)
+    bad = (full.view(np.uint8).reshape(n, -1) != ref.view(np.uint8).reshape(n, -1)).any(axis=1)
+    assert not bad.any(), f"{int(bad.sum())} records differ from the oracle, first {np.nonzero(bad)[0][:5]}"
+
+
+def test_park_slots_run_out(orc):
+    """Fewer park slots than overflowing pairs: the rest restart from the simplex, same records."""
+    n = 4000
+    pool = gjkepa.synth_pairs(SEED + 1, n, 129, 256, 0.6)
+    minimum = (512 + n + 255) // 256 * 256
+    few, parked = _run(pool, minimum + 5 * 2880)           # five slots
+    assert parked > 5                                      # the counter runs past the capacity
+    ref = orc.gjkepa_batch(pool, 2, 1.0)
+    assert few.tobytes() == ref.tobytes()
+
+
+def test_parked_fp32_chain_matches_unparked():
+    n = 4000
+    pool = gjkepa.synth_pairs(SEED + 2, n, 129, 256, 0.6)
+    full, parked = _run(pool, gjkepa.workspace_bytes(n), gjkepa.PREC_F32)
+    bare, _ = _run(pool, (512 + n + 255) // 256 * 256, gjkepa.PREC_F32)
+    assert parked > 0
+    assert full.tobytes() == bare.tobytes()

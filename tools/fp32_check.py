@@ -37,7 +37,7 @@ def model_fp32(pool, r64, threads):
 
 
 def main():
-    cfgs = [a for a in sys.argv[1:] if a.startswith("C")] or ["C2", "C5"]
+    cfgs = [a for a in sys.argv[1:] if a.startswith("C")] or ["C2", "C5", "C4"]
     npairs = int(sys.argv[sys.argv.index("--pairs") + 1]) if "--pairs" in sys.argv else 0
     threads = host_cpus()["usable"]
     for cfg in cfgs:

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 echo "== fp32 check $(date)"
-timeout -k 10 400 python -u tools/fp32_check.py C2 C5 > $OUT/fp32_check.log 2>&1; rc=$?
+timeout -k 10 400 python -u tools/fp32_check.py C2 C5 C4 > $OUT/fp32_check.log 2>&1; rc=$?
 cut -c1-1200 $OUT/fp32_check.log; [ $rc -eq 0 ] || exit $rc
 if [ "$2" != "skip-tests" ]; then
   echo "== tests $(date)"
