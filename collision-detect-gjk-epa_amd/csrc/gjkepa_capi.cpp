@@ -159,6 +159,7 @@ struct Fork {
     std::mutex mu;
     hipStream_t s2[GJKEPA_EPA_TIERS] = {};       // internal stream of fork point t (all [0] if shared)
     hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join[GJKEPA_EPA_TIERS] = {};
+    hipEvent_t part[8] = {};                     // fork of EPA tier 0's part i (kEpa0PartsMax)
 };
 struct ForkKey {
     int dev;
@@ -190,6 +191,7 @@ int fork_state(hipStream_t s, Fork** out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork[t], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[t], hipEventDisableTiming);
     }
+    for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&f->part[i], hipEventDisableTiming);
     if (e != hipSuccess) {
         delete f;
         return hip_fail(e, "overlap stream / events");
@@ -223,12 +225,28 @@ constexpr int fork_contact_tiers(int p) {
         if (fork_point(t) == p && epa_hull_cap(t) > cap) cap = epa_hull_cap(t);
     return cap <= GJKEPA_C0_G * GJKEPA_C0_K ? 1 : GJKEPA_CONTACT_TIERS;
 }
-// launches of an overlapped chain: 2 GJK + the EPA tiers + each fork point's contact pass; every
-// launch owns one workspace counter
+// EPA tier 0 in parts (GJKEPA_EPA0_PARTS; environment override for A/B): tier 0 runs over P
+// consecutive pair ranges, one launch each, and the contact pass of part i is forked as soon as part i
+// is done, so it runs beside the EPA of parts i+1.. instead of after all of tier 0 (C2's critical path
+// was GJK 0 -> EPA 0 -> the whole contact pass).  Which launch answers a pair never changes its record.
+#ifndef GJKEPA_EPA0_PARTS
+#define GJKEPA_EPA0_PARTS 4
+#endif
+constexpr int kEpa0PartsMax = 8;
+int epa0_parts() {
+    static const int p = [] {
+        const char* e = std::getenv("GJKEPA_EPA0_PARTS");
+        int v = e ? std::atoi(e) : GJKEPA_EPA0_PARTS;
+        return v < 1 ? 1 : v > kEpa0PartsMax ? kEpa0PartsMax : v;
+    }();
+    return p;
+}
+// launches of an overlapped chain: 2 GJK + the EPA tiers (tier 0 in up to kEpa0PartsMax parts) + each
+// fork point's contact pass (tier 0's once per part); every launch owns one workspace counter
 constexpr int overlap_launches() {
-    int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS;
+    int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS + (kEpa0PartsMax - 1);
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
-        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t);
+        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t) * (t == 0 ? kEpa0PartsMax : 1);
     return n;
 }
 static_assert(overlap_launches() + 1 <= GJKEPA_WS_COUNTERS, "workspace launch counters (+1: the fp32 redo launch)");
@@ -318,6 +336,13 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     int rc;
     if (GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin && (rc = fork_state(s, &f))) return rc;
     const bool overlap = f != nullptr;
+    const gjkepa_epa_args whole = a;                     // (a.pairs / route / out / n_pairs: a pair range below)
+    auto range = [&](int64_t first, int64_t count) {     // point `a` at pairs [first, first + count)
+        a.pairs = whole.pairs + 2 * first;
+        a.route = whole.route + first;
+        a.out = (unsigned char*)whole.out + first * (precision == GJKEPA_PREC_F64 ? 128 : 64);
+        a.n_pairs = count;
+    };
     auto epa_tier = [&](int t) -> int {                  // EPA tier t; polytope overflow -> t+1
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
         a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
@@ -361,7 +386,23 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         std::lock_guard<std::mutex> lk(f->mu);
         constexpr int last = GJKEPA_EPA_TIERS - 1;
         bool forked[GJKEPA_EPA_TIERS] = {};
-        for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
+        const int parts = (GJKEPA_FORK_MASK & 1) && !(GJKEPA_LAST_PASS_MAIN && last == 0) ? epa0_parts() : 1;
+        if (parts > 1) {                                  // EPA tier 0 in parts, each part's contact pass forked
+            const int64_t chunks = (n_pairs + 63) / 64;
+            for (int i = 0; i < parts; ++i) {
+                const int64_t c0 = chunks * i / parts, c1 = chunks * (i + 1) / parts;
+                const int64_t first = c0 * 64, count = (c1 * 64 < n_pairs ? c1 * 64 : n_pairs) - first;
+                if (count <= 0) continue;
+                range(first, count);
+                if ((rc = epa_tier(0))) return rc;
+                if ((e = hipEventRecord(f->part[i], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[0], f->part[i], 0)) != hipSuccess)
+                    return hip_fail(e, "contact pass fork");
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(0), fork_contact_tiers(0), f->s2[0]))) return rc;
+            }
+            a = whole;
+            forked[0] = true;
+        }
+        for (int t = parts > 1 ? 1 : 0; t < GJKEPA_EPA_TIERS; ++t) {
             if ((rc = epa_tier(t))) return rc;
             if (!((GJKEPA_FORK_MASK >> t) & 1)) continue;
             if (GJKEPA_LAST_PASS_MAIN && t == last) {

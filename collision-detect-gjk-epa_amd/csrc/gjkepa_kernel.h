@@ -231,8 +231,9 @@
 #define GJKEPA_EPA_TIERS 6
 #define GJKEPA_CONTACT_TIERS 2
 
-// workspace: a 256-byte header of per-launch chunk counters, then one route byte per pair
-#define GJKEPA_WS_COUNTERS 16   // uint32 counters at the head of the workspace (at most 15 launches used)
+// workspace: a 512-byte header of per-launch chunk counters, route tallies and the park counter, then
+// one route byte per pair, then park slots (gjkepa_capi.cpp, gjkepa_workspace_bytes)
+#define GJKEPA_WS_COUNTERS 32   // uint32 counters at the head of the workspace (one per launch of a chain)
 // then GJKEPA_WS_TALLY uint32 route tallies (indexed by route code): every kernel adds the pairs it
 // routes on; a launch whose own tally is at least 1/16 of the batch claims single chunks (dense),
 // otherwise runs of `claim` chunks (sparse scan)

@@ -11,5 +11,5 @@ F="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $*"
 /opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_kernel.hip -o $OUT/k.o
 /opt/rocm/bin/hipcc $F -DGJKEPA_SRC_HASH="\"variant-$NAME\"" -c $D/csrc/gjkepa_capi.cpp -o $OUT/c.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k.o $OUT/c.o $D/build/hull_kernel.o \
-    $D/build/broadphase_kernel.o $D/build/contacts_kernel.o $D/build/gjkepa_multi.o $D/build/synth.o -o $OUT/libgjkepa_hip.so
+    $D/build/broadphase_kernel.o $D/build/contacts_kernel.o $D/build/gjkepa_multi.o $D/build/synth.o -o $OUT/libgjkepa_hip.so -ldl -pthread -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo built $OUT/libgjkepa_hip.so
