@@ -230,7 +230,7 @@ constexpr int fork_contact_tiers(int p) {
 // is done, so it runs beside the EPA of parts i+1.. instead of after all of tier 0 (C2's critical path
 // was GJK 0 -> EPA 0 -> the whole contact pass).  Which launch answers a pair never changes its record.
 #ifndef GJKEPA_EPA0_PARTS
-#define GJKEPA_EPA0_PARTS 4
+#define GJKEPA_EPA0_PARTS 2       // A/B r4 (C2, 2 rounds): 1 part 149.7, 2 parts 150.7, 4 parts 145.5, 8 parts 113.8 M/s
 #endif
 constexpr int kEpa0PartsMax = 8;
 int epa0_parts() {

@@ -26,7 +26,8 @@ def _run(pool, ws_bytes, precision=gjkepa.PREC_F64):
     gjkepa.gjkepa_batch_device(2, 1.0, pool.dtype_code, precision, v.data_ptr(), o.data_ptr(), c.data_ptr(),
                                p.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes, 0)
     torch.cuda.synchronize()
-    parked = int(ws[64 * 4:65 * 4].cpu().numpy().view(np.uint32)[0])     # header word 64: park slots taken
+    w = gjkepa.WS_PARK_WORD                                          # header word: park slots taken
+    parked = int(ws[w * 4:(w + 1) * 4].cpu().numpy().view(np.uint32)[0])
     return np.frombuffer(out.cpu().numpy().tobytes(), gjkepa.record_dtype(precision)), parked
 
 

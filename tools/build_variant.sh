@@ -5,7 +5,7 @@
 set -e
 NAME=$1; shift
 D=collision-detect-gjk-epa_amd
-OUT=$D/build/variants/$NAME
+OUT=${VARDIR:-$D/build/variants}/$NAME
 mkdir -p $OUT
 F="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $*"
 /opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_kernel.hip -o $OUT/k.o

@@ -10,3 +10,7 @@ B=tests/fortran/build/bench_callpattern
 OMP_NUM_THREADS=1 GJKEPA_QUERY_STATS=1 timeout -k 10 200 $B $N1 > $OUT/cp1.txt 2>&1 && cat $OUT/cp1.txt && \
 OMP_NUM_THREADS=16 GJKEPA_QUERY_STATS=1 timeout -k 10 200 $B $N16 > $OUT/cp16.txt 2>&1 && cat $OUT/cp16.txt && \
 OMP_NUM_THREADS=64 GJKEPA_QUERY_STATS=1 timeout -k 10 200 $B $N16 > $OUT/cp64.txt 2>&1 && cat $OUT/cp64.txt
+# the 64-thread run again with passive OpenMP waiting: after the parallel loop, 63 idle OpenMP threads
+# no longer spin on the 16-CPU share while the master runs GJKEPA_BATCH (the suspected cause of its
+# 3x slowdown in round 3)
+OMP_NUM_THREADS=64 OMP_WAIT_POLICY=passive GJKEPA_QUERY_STATS=1 timeout -k 10 200 $B $N16 > $OUT/cp64p.txt 2>&1 && cat $OUT/cp64p.txt
