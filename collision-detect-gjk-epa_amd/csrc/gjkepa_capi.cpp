@@ -160,6 +160,8 @@ struct Fork {
     hipStream_t s2[GJKEPA_EPA_TIERS] = {};       // internal stream of fork point t (all [0] if shared)
     hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join[GJKEPA_EPA_TIERS] = {};
     hipEvent_t part[8] = {};                     // fork of EPA tier 0's part i (kEpa0PartsMax)
+    hipStream_t s3 = nullptr;                    // second stream for alternate parts (GJKEPA_EPA0_STREAMS 2)
+    hipEvent_t fork3 = nullptr, join3 = nullptr;
 };
 struct ForkKey {
     int dev;
@@ -192,6 +194,9 @@ int fork_state(hipStream_t s, Fork** out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[t], hipEventDisableTiming);
     }
     for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&f->part[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&f->s3, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork3, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join3, hipEventDisableTiming);
     if (e != hipSuccess) {
         delete f;
         return hip_fail(e, "overlap stream / events");
@@ -233,6 +238,15 @@ constexpr int fork_contact_tiers(int p) {
 #define GJKEPA_EPA0_PARTS 2       // A/B r4 (C2, 2 rounds): 1 part 149.7, 2 parts 150.7, 4 parts 145.5, 8 parts 113.8 M/s
 #endif
 constexpr int kEpa0PartsMax = 8;
+// the parts alternate between the caller's stream and a second internal stream (2), so a part's tail
+// overlaps the next part instead of idling the CUs it leaves (GJKEPA_EPA0_STREAMS, environment A/B)
+int epa0_streams() {
+    static const int p = [] {
+        const char* e = std::getenv("GJKEPA_EPA0_STREAMS");
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
+    return p;
+}
 int epa0_parts() {
     static const int p = [] {
         const char* e = std::getenv("GJKEPA_EPA0_PARTS");
@@ -389,16 +403,29 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         const int parts = (GJKEPA_FORK_MASK & 1) && !(GJKEPA_LAST_PASS_MAIN && last == 0) ? epa0_parts() : 1;
         if (parts > 1) {                                  // EPA tier 0 in parts, each part's contact pass forked
             const int64_t chunks = (n_pairs + 63) / 64;
+            const bool two = epa0_streams() == 2;
+            if (two && ((e = hipEventRecord(f->fork3, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s3, f->fork3, 0)) != hipSuccess))
+                return hip_fail(e, "EPA part stream fork");
             for (int i = 0; i < parts; ++i) {
                 const int64_t c0 = chunks * i / parts, c1 = chunks * (i + 1) / parts;
                 const int64_t first = c0 * 64, count = (c1 * 64 < n_pairs ? c1 * 64 : n_pairs) - first;
                 if (count <= 0) continue;
                 range(first, count);
-                if ((rc = epa_tier(0))) return rc;
-                if ((e = hipEventRecord(f->part[i], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[0], f->part[i], 0)) != hipSuccess)
+                hipStream_t ps = two && (i & 1) ? f->s3 : s;
+                a.route_code = GJKEPA_ROUTE_EPA0;
+                a.next_code = GJKEPA_ROUTE_EPA0 + 1;
+                a.ct_base = GJKEPA_ROUTE_CT(fork_point(0));
+                a.ctr = ctr + launch++;
+                a.claim = 1;
+                a.grid = 0;
+                a.guard = gjkepa_guard_of(a);
+                if ((e = gjkepa_launch_epa(0, vert_dtype, precision, a, ps)) != hipSuccess) return hip_fail(e, "EPA tier launch");
+                if ((e = hipEventRecord(f->part[i], ps)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[0], f->part[i], 0)) != hipSuccess)
                     return hip_fail(e, "contact pass fork");
                 if ((rc = contact_tiers(GJKEPA_ROUTE_CT(0), fork_contact_tiers(0), f->s2[0]))) return rc;
             }
+            if (two && ((e = hipEventRecord(f->join3, f->s3)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join3, 0)) != hipSuccess))
+                return hip_fail(e, "EPA part stream join");
             a = whole;
             forked[0] = true;
         }
