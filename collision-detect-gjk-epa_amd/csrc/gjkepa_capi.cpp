@@ -240,10 +240,14 @@ constexpr int fork_contact_tiers(int p) {
 constexpr int kEpa0PartsMax = 8;
 // the parts alternate between the caller's stream and a second internal stream (2), so a part's tail
 // overlaps the next part instead of idling the CUs it leaves (GJKEPA_EPA0_STREAMS, environment A/B)
+#ifndef GJKEPA_EPA0_STREAMS
+#define GJKEPA_EPA0_STREAMS 2     // A/B r4 (C2, 2 rounds, 2 parts): one stream 150.7, two streams 157.4 M/s
+#endif
 int epa0_streams() {
     static const int p = [] {
         const char* e = std::getenv("GJKEPA_EPA0_STREAMS");
-        return e && std::atoi(e) == 2 ? 2 : 1;
+        const int v = e ? std::atoi(e) : GJKEPA_EPA0_STREAMS;
+        return v == 2 ? 2 : 1;
     }();
     return p;
 }
