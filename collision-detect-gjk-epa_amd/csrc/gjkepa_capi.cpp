@@ -740,7 +740,13 @@ struct Service {
     std::atomic<uint64_t> free_slots{~0ull >> (64 - GJKEPA_SVC_SLOTS)};
     uint32_t seq[GJKEPA_SVC_SLOTS] = {};      // last posted sequence number, owned by the slot's holder
     uint64_t idle_ticks = 0, life_ticks = 0;
+    // grid size: slots 0..grid_n-1 have a wave.  Each launch sizes the grid to the slots claimed since
+    // the previous one (callers take the lowest free slot, so that is the recent concurrency), in
+    // steps of kSvcGridStep; a caller whose slot has no wave stops the grid and relaunches it larger.
+    std::atomic<int> grid_n{0};
+    std::atomic<int> hi{0};                   // highest slot + 1 claimed since the last launch
 };
+constexpr int kSvcGridStep = 8;
 static_assert(GJKEPA_SVC_SLOTS >= 1 && GJKEPA_SVC_SLOTS <= 64, "service slot bitmap");
 std::mutex g_svc_mu;
 std::vector<Service*> g_svc;
@@ -829,32 +835,46 @@ Service* service(int device) {
     return sv;
 }
 
-// make sure a grid newer than `seen` (or any grid, seen == 0) is serving: relaunch when none was
-// launched, the latest one is draining (it wrote its generation to `closing`), or `check_done` and
-// the latest one has finished
-int service_ensure(Service* sv, bool check_done) {
+// make sure a grid that serves `slot` is running: relaunch when none was launched, the latest one is
+// draining (it wrote its generation to `closing`), `check_done` and the latest one has finished, or
+// the latest one has no wave for `slot` (it is stopped and relaunched larger)
+int service_ensure(Service* sv, bool check_done, int slot) {
     const uint32_t g0 = sv->gen.load(std::memory_order_acquire);
-    if (g0 != 0 && __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) != g0 && !check_done) return 0;
+    const bool small = g0 != 0 && slot >= sv->grid_n.load(std::memory_order_acquire);
+    if (g0 != 0 && __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) != g0 && !check_done && !small) return 0;
     std::lock_guard<std::mutex> g(sv->mu);
     const uint32_t g1 = sv->gen.load(std::memory_order_relaxed);
-    if (g1 != g0) return 0;                   // another caller relaunched meanwhile
+    if (g1 != g0) return 0;                   // another caller relaunched meanwhile (a small one: next poll)
     hipError_t e;
     if (g1 != 0) {
-        bool need = __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) == g1;
+        bool need = __atomic_load_n(sv->closing, __ATOMIC_ACQUIRE) == g1 || small;
         if (!need && check_done) {
             e = hipEventQuery(sv->ev);
             if (e != hipSuccess && e != hipErrorNotReady) return hip_fail(e, "query service");
             need = e == hipSuccess;
         }
         if (!need) return 0;
-        if ((e = hipEventSynchronize(sv->ev)) != hipSuccess) return hip_fail(e, "query service drain");
+        // a grid too small for this slot leaves once its waves have answered what they hold
+        if (small) for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 1u, __ATOMIC_RELEASE);
+        e = hipEventSynchronize(sv->ev);
+        if (small) for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 0u, __ATOMIC_RELEASE);
+        if (e != hipSuccess) return hip_fail(e, "query service drain");
     }
     if ((e = hipSetDevice(sv->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
     uint32_t ng = g1 + 1;
     if (ng == 0) ng = 1;
+    // size: the slots claimed since the last launch and now, and this one, rounded up to the step
+    const uint64_t claimed = ~sv->free_slots.load(std::memory_order_acquire) & (~0ull >> (64 - GJKEPA_SVC_SLOTS));
+    int want = sv->hi.exchange(claimed ? 64 - __builtin_clzll(claimed) : 0, std::memory_order_relaxed);
+    const int now = claimed ? 64 - __builtin_clzll(claimed) : 0;
+    want = want > now ? want : now;
+    want = want > slot + 1 ? want : slot + 1;
+    int n = (want + kSvcGridStep - 1) / kSvcGridStep * kSvcGridStep;
+    n = n < kSvcGridStep ? kSvcGridStep : n > GJKEPA_SVC_SLOTS ? GJKEPA_SVC_SLOTS : n;
     gjkepa_svc_args a{sv->dslots, sv->ctrl, sv->dclosing, ng, sv->idle_ticks, sv->life_ticks};
-    if ((e = gjkepa_launch_service(a, GJKEPA_SVC_SLOTS, sv->stream)) != hipSuccess) return hip_fail(e, "query service launch");
+    if ((e = gjkepa_launch_service(a, n, sv->stream)) != hipSuccess) return hip_fail(e, "query service launch");
     if ((e = hipEventRecord(sv->ev, sv->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    sv->grid_n.store(n, std::memory_order_release);
     sv->gen.store(ng, std::memory_order_release);
     return 0;
 }
@@ -875,7 +895,12 @@ int service_claim(Service* sv) {
     uint64_t f = sv->free_slots.load(std::memory_order_relaxed);
     while (f) {
         const int k = __builtin_ctzll(f);
-        if (sv->free_slots.compare_exchange_weak(f, f & ~(1ull << k), std::memory_order_acquire)) return k;
+        if (sv->free_slots.compare_exchange_weak(f, f & ~(1ull << k), std::memory_order_acquire)) {
+            int h = sv->hi.load(std::memory_order_relaxed);
+            while (h < k + 1 && !sv->hi.compare_exchange_weak(h, k + 1, std::memory_order_relaxed)) {
+            }
+            return k;
+        }
     }
     return -1;
 }
@@ -894,7 +919,7 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
     if (seq == 0) seq = 1;
     sv->seq[k] = seq;
     __atomic_store_n(&sl->req, seq, __ATOMIC_RELEASE);
-    int rc = service_ensure(sv, false);
+    int rc = service_ensure(sv, false, k);
     if (rc) return rc;
     const auto t0 = std::chrono::steady_clock::now();
     auto next_check = t0 + std::chrono::microseconds(200);
@@ -908,9 +933,9 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
             const auto now = std::chrono::steady_clock::now();
             yield = now - t0 > std::chrono::microseconds(80);
             // a grid that reached its idle or lifetime limit marks itself closing: relaunch at once
-            if ((rc = service_ensure(sv, false)) != 0) return rc;
+            if ((rc = service_ensure(sv, false, k)) != 0) return rc;
             if (now >= next_check) {              // the grid may have drained under this request
-                if ((rc = service_ensure(sv, true)) != 0) return rc;
+                if ((rc = service_ensure(sv, true, k)) != 0) return rc;
                 next_check = now + std::chrono::microseconds(200);
                 if (now - t0 > std::chrono::seconds(30)) return fail(GJKEPA_E_HIP, "query service: no answer in 30 s");
             }
