@@ -367,7 +367,10 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         a.ct_base = overlap ? GJKEPA_ROUTE_CT(fork_point(t)) : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
-        a.grid = 0;
+        // the last tier (overflow of the 208-face polytope: rare) takes one workgroup per CU: its
+        // one-wave-per-SIMD workgroups otherwise queue for dispatch behind a concurrent contact pass even
+        // when the tier is empty (C5: an empty launch spanned 1.1 ms of the chain)
+        a.grid = t == GJKEPA_EPA_TIERS - 1 ? num_cus : 0;
         a.guard = gjkepa_guard_of(a);
         hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, s);
         return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");

@@ -32,7 +32,7 @@
 #define GJKEPA_G1_K 8
 #endif
 #ifndef GJKEPA_G1_MINW
-#define GJKEPA_G1_MINW 2
+#define GJKEPA_G1_MINW 3           // LDS hull frees the 96 VGPRs of register copies: three waves per SIMD
 #endif
 // EPA tiers: G, K as above, EPA polytope capacity VCAP vertices / FCAP faces
 #ifndef GJKEPA_E0_G
@@ -198,7 +198,7 @@
 #define GJKEPA_G0_LH 1
 #endif
 #ifndef GJKEPA_G1_LH
-#define GJKEPA_G1_LH 0
+#define GJKEPA_G1_LH 1             // A/B r4 (2 rounds, with G1_MINW 3): C4 39.07 -> 39.54, C2 -0.2%, C5 -0.4%
 #endif
 #ifndef GJKEPA_E0_LH
 #define GJKEPA_E0_LH 1
