@@ -25,5 +25,5 @@ done
 echo "== pmc C2 $(date)" && timeout -k 10 600 bash tools/pmc.sh $TAG > $OUT/pmc.log 2>&1 && cat $OUT/pmc.log || exit 1
 echo "== pmc C5 $(date)" && timeout -k 10 600 bash tools/pmc.sh ${TAG}_c5 --config C5 > $OUT/pmc_c5.log 2>&1 && cat $OUT/pmc_c5.log || exit 1
 echo "== call pattern $(date)" && timeout -k 10 700 bash tools/callpattern_probe.sh $TAG/callpattern 5000 100000 || exit 1
-echo "== service concurrency $(date)" && timeout -k 10 300 python tools/svc_concurrent.py 4 16 > $OUT/svc_concurrent.json 2>&1 && cat $OUT/svc_concurrent.json || exit 1
+echo "== service concurrency $(date)" && timeout -k 10 300 python tools/svc_concurrent.py 1 4 16 > $OUT/svc_concurrent.json 2>&1 && cat $OUT/svc_concurrent.json || exit 1
 echo "== done $(date)"
