@@ -159,7 +159,7 @@ struct Fork {
     std::mutex mu;
     hipStream_t s2[GJKEPA_EPA_TIERS] = {};       // internal stream of fork point t (all [0] if shared)
     hipEvent_t fork[GJKEPA_EPA_TIERS] = {}, join[GJKEPA_EPA_TIERS] = {};
-    hipEvent_t part[8] = {};                     // fork of EPA tier 0's part i (kEpa0PartsMax)
+    hipEvent_t part[8] = {};                     // fork of EPA tier 0's (0..3) / tier 2's (4..7) part i
     hipStream_t s3 = nullptr;                    // second stream for alternate parts (GJKEPA_EPA0_STREAMS 2)
     hipEvent_t fork3 = nullptr, join3 = nullptr;
 };
@@ -237,7 +237,12 @@ constexpr int fork_contact_tiers(int p) {
 #ifndef GJKEPA_EPA0_PARTS
 #define GJKEPA_EPA0_PARTS 2       // A/B r4 (C2, 2 rounds): 1 part 149.7, 2 parts 150.7, 4 parts 145.5, 8 parts 113.8 M/s
 #endif
-constexpr int kEpa0PartsMax = 8;
+constexpr int kPartsMax = 4;
+int parts_env(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : dflt;
+    return v < 1 ? 1 : v > kPartsMax ? kPartsMax : v;
+}
 // the parts alternate between the caller's stream and a second internal stream (2), so a part's tail
 // overlaps the next part instead of idling the CUs it leaves (GJKEPA_EPA0_STREAMS, environment A/B)
 #ifndef GJKEPA_EPA0_STREAMS
@@ -252,19 +257,23 @@ int epa0_streams() {
     return p;
 }
 int epa0_parts() {
-    static const int p = [] {
-        const char* e = std::getenv("GJKEPA_EPA0_PARTS");
-        int v = e ? std::atoi(e) : GJKEPA_EPA0_PARTS;
-        return v < 1 ? 1 : v > kEpa0PartsMax ? kEpa0PartsMax : v;
-    }();
+    static const int p = parts_env("GJKEPA_EPA0_PARTS", GJKEPA_EPA0_PARTS);
     return p;
 }
-// launches of an overlapped chain: 2 GJK + the EPA tiers (tier 0 in up to kEpa0PartsMax parts) + each
-// fork point's contact pass (tier 0's once per part); every launch owns one workspace counter
+// EPA tier 2 (hulls of 33-128 vertices: most of C5's pairs) in parts the same way (GJKEPA_EPA2_PARTS)
+#ifndef GJKEPA_EPA2_PARTS
+#define GJKEPA_EPA2_PARTS 1
+#endif
+int epa2_parts() {
+    static const int p = parts_env("GJKEPA_EPA2_PARTS", GJKEPA_EPA2_PARTS);
+    return p;
+}
+// launches of an overlapped chain: 2 GJK + the EPA tiers (tiers 0 and 2 in up to kPartsMax parts) +
+// each fork point's contact pass (once per part); every launch owns one workspace counter
 constexpr int overlap_launches() {
-    int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS + (kEpa0PartsMax - 1);
+    int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS + 2 * (kPartsMax - 1);
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
-        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t) * (t == 0 ? kEpa0PartsMax : 1);
+        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t) * (t == 0 || t == 2 ? kPartsMax : 1);
     return n;
 }
 static_assert(overlap_launches() + 1 <= GJKEPA_WS_COUNTERS, "workspace launch counters (+1: the fp32 redo launch)");
@@ -407,8 +416,9 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         std::lock_guard<std::mutex> lk(f->mu);
         constexpr int last = GJKEPA_EPA_TIERS - 1;
         bool forked[GJKEPA_EPA_TIERS] = {};
-        const int parts = (GJKEPA_FORK_MASK & 1) && !(GJKEPA_LAST_PASS_MAIN && last == 0) ? epa0_parts() : 1;
-        if (parts > 1) {                                  // EPA tier 0 in parts, each part's contact pass forked
+        // EPA tier t (a fork point that forks) in `parts` launches over consecutive pair ranges, alternately
+        // on the caller's stream and an internal one, each range's contact pass forked when it is done
+        auto parted = [&](int t, int parts) -> int {
             const int64_t chunks = (n_pairs + 63) / 64;
             const bool two = epa0_streams() == 2;
             if (two && ((e = hipEventRecord(f->fork3, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s3, f->fork3, 0)) != hipSuccess))
@@ -419,24 +429,32 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
                 if (count <= 0) continue;
                 range(first, count);
                 hipStream_t ps = two && (i & 1) ? f->s3 : s;
-                a.route_code = GJKEPA_ROUTE_EPA0;
-                a.next_code = GJKEPA_ROUTE_EPA0 + 1;
-                a.ct_base = GJKEPA_ROUTE_CT(fork_point(0));
+                a.route_code = GJKEPA_ROUTE_EPA0 + t;
+                a.next_code = GJKEPA_ROUTE_EPA0 + t + 1;
+                a.ct_base = GJKEPA_ROUTE_CT(fork_point(t));
                 a.ctr = ctr + launch++;
-                a.claim = 1;
+                a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
                 a.grid = 0;
                 a.guard = gjkepa_guard_of(a);
-                if ((e = gjkepa_launch_epa(0, vert_dtype, precision, a, ps)) != hipSuccess) return hip_fail(e, "EPA tier launch");
-                if ((e = hipEventRecord(f->part[i], ps)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[0], f->part[i], 0)) != hipSuccess)
+                if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, ps)) != hipSuccess) return hip_fail(e, "EPA tier launch");
+                hipEvent_t pe = f->part[(t == 0 ? 0 : kPartsMax) + i];
+                if ((e = hipEventRecord(pe, ps)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[t], pe, 0)) != hipSuccess)
                     return hip_fail(e, "contact pass fork");
-                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(0), fork_contact_tiers(0), f->s2[0]))) return rc;
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), f->s2[t]))) return rc;
             }
             if (two && ((e = hipEventRecord(f->join3, f->s3)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join3, 0)) != hipSuccess))
                 return hip_fail(e, "EPA part stream join");
             a = whole;
-            forked[0] = true;
-        }
-        for (int t = parts > 1 ? 1 : 0; t < GJKEPA_EPA_TIERS; ++t) {
+            forked[t] = true;
+            return 0;
+        };
+        for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
+            const bool forks = ((GJKEPA_FORK_MASK >> t) & 1) && !(GJKEPA_LAST_PASS_MAIN && t == last);
+            const int np = !forks ? 1 : t == 0 ? epa0_parts() : t == 2 ? epa2_parts() : 1;
+            if (np > 1) {
+                if ((rc = parted(t, np))) return rc;
+                continue;
+            }
             if ((rc = epa_tier(t))) return rc;
             if (!((GJKEPA_FORK_MASK >> t) & 1)) continue;
             if (GJKEPA_LAST_PASS_MAIN && t == last) {
