@@ -162,6 +162,8 @@ struct Fork {
     hipEvent_t part[8] = {};                     // fork of EPA tier 0's (0..3) / tier 2's (4..7) part i
     hipStream_t s3 = nullptr;                    // second stream for alternate parts (GJKEPA_EPA0_STREAMS 2)
     hipEvent_t fork3 = nullptr, join3 = nullptr;
+    hipStream_t s4 = nullptr;                    // contact passes of the odd parts (GJKEPA_PART_PASS_STREAMS 2)
+    hipEvent_t join4 = nullptr;
 };
 struct ForkKey {
     int dev;
@@ -197,6 +199,8 @@ int fork_state(hipStream_t s, Fork** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&f->s3, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork3, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join3, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&f->s4, hipStreamNonBlocking, prio);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join4, hipEventDisableTiming);
     if (e != hipSuccess) {
         delete f;
         return hip_fail(e, "overlap stream / events");
@@ -252,6 +256,19 @@ int epa0_streams() {
     static const int p = [] {
         const char* e = std::getenv("GJKEPA_EPA0_STREAMS");
         const int v = e ? std::atoi(e) : GJKEPA_EPA0_STREAMS;
+        return v == 2 ? 2 : 1;
+    }();
+    return p;
+}
+// the contact passes of the odd parts on their own internal stream (2), so a part's pass starts when
+// its EPA part ends instead of queueing behind the previous part's pass (GJKEPA_PART_PASS_STREAMS)
+#ifndef GJKEPA_PART_PASS_STREAMS
+#define GJKEPA_PART_PASS_STREAMS 1
+#endif
+int part_pass_streams() {
+    static const int p = [] {
+        const char* e = std::getenv("GJKEPA_PART_PASS_STREAMS");
+        const int v = e ? std::atoi(e) : GJKEPA_PART_PASS_STREAMS;
         return v == 2 ? 2 : 1;
     }();
     return p;
@@ -418,6 +435,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         bool forked[GJKEPA_EPA_TIERS] = {};
         // EPA tier t (a fork point that forks) in `parts` launches over consecutive pair ranges, alternately
         // on the caller's stream and an internal one, each range's contact pass forked when it is done
+        bool used4 = false;
         auto parted = [&](int t, int parts) -> int {
             const int64_t chunks = (n_pairs + 63) / 64;
             const bool two = epa0_streams() == 2;
@@ -438,9 +456,11 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
                 a.guard = gjkepa_guard_of(a);
                 if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, ps)) != hipSuccess) return hip_fail(e, "EPA tier launch");
                 hipEvent_t pe = f->part[(t == 0 ? 0 : kPartsMax) + i];
-                if ((e = hipEventRecord(pe, ps)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[t], pe, 0)) != hipSuccess)
+                hipStream_t cs = part_pass_streams() == 2 && (i & 1) ? f->s4 : f->s2[t];
+                if ((e = hipEventRecord(pe, ps)) != hipSuccess || (e = hipStreamWaitEvent(cs, pe, 0)) != hipSuccess)
                     return hip_fail(e, "contact pass fork");
-                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), f->s2[t]))) return rc;
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), cs))) return rc;
+                if (cs == f->s4) used4 = true;
             }
             if (two && ((e = hipEventRecord(f->join3, f->s3)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join3, 0)) != hipSuccess))
                 return hip_fail(e, "EPA part stream join");
@@ -474,6 +494,8 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             if ((e = hipEventRecord(f->join[t], f->s2[t])) != hipSuccess || (e = hipStreamWaitEvent(s, f->join[t], 0)) != hipSuccess)
                 return hip_fail(e, "contact pass join");
         }
+        if (used4 && ((e = hipEventRecord(f->join4, f->s4)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join4, 0)) != hipSuccess))
+            return hip_fail(e, "contact pass join");
         return redo();
     }
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
