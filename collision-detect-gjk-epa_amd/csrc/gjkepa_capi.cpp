@@ -273,6 +273,19 @@ int part_pass_streams() {
     }();
     return p;
 }
+// share of the pair range in EPA tier 0's first part when it runs in two (per mille; environment
+// GJKEPA_EPA0_FIRST, A/B): the second part's contact pass is the chain's tail
+#ifndef GJKEPA_EPA0_FIRST
+#define GJKEPA_EPA0_FIRST 650      // A/B r4 (C2, 5 rounds): 500 157.6, 650 158.6, 700-750 158.5, 300 151.7 M/s
+#endif
+int epa0_first() {
+    static const int p = [] {
+        const char* e = std::getenv("GJKEPA_EPA0_FIRST");
+        const int v = e ? std::atoi(e) : GJKEPA_EPA0_FIRST;
+        return v < 100 ? 100 : v > 900 ? 900 : v;
+    }();
+    return p;
+}
 int epa0_parts() {
     static const int p = parts_env("GJKEPA_EPA0_PARTS", GJKEPA_EPA0_PARTS);
     return p;
@@ -442,7 +455,12 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             if (two && ((e = hipEventRecord(f->fork3, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s3, f->fork3, 0)) != hipSuccess))
                 return hip_fail(e, "EPA part stream fork");
             for (int i = 0; i < parts; ++i) {
-                const int64_t c0 = chunks * i / parts, c1 = chunks * (i + 1) / parts;
+                int64_t c0 = chunks * i / parts, c1 = chunks * (i + 1) / parts;
+                if (t == 0 && parts == 2) {                  // uneven halves (GJKEPA_EPA0_FIRST)
+                    const int64_t cut = chunks * epa0_first() / 1000;
+                    c0 = i == 0 ? 0 : cut;
+                    c1 = i == 0 ? cut : chunks;
+                }
                 const int64_t first = c0 * 64, count = (c1 * 64 < n_pairs ? c1 * 64 : n_pairs) - first;
                 if (count <= 0) continue;
                 range(first, count);

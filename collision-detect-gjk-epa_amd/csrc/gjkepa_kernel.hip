@@ -987,7 +987,6 @@ CTX_T DEV int epa_seed(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s
 // Closes iteration S.iters (MINLOC of the polytope, termination :956-1015); if EPA goes on, the
 // next iteration's direction (:888-910) replaces S.dir.  ST_CONT, 0 (depth and normal set) or a status.
 CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
-    const V3<T> O = zero3<T>();
     const int F2 = S.nf;                                      // :956-969
     const T prev = S.minv;
     face_argmin(c, S.F, S.minv, S.dir, S.neg, S.av);
