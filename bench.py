@@ -14,9 +14,16 @@ region ends after the last gather has completed, so every step's exchange is ins
 torch.distributed (gloo) is the control plane only: RCCL id broadcast, barriers, max over ranks.
 `--backend gloo` is the one-GPU rehearsal: ranks may share a device, records gathered via host.
 
-Extra legs (not timed in `value`): the roofline of the dominant kernel from HIP events on the
-launch stream, and on rank 0 at N=1 a CPU baseline — the oracle restatement (kind "port") over a
-bounded sample of the same pairs, which also re-checks GPU/CPU parity on that sample.
+The roofline is the dominant kernel's: the library's launch timing (gjkepa_launch_timing: HIP events
+recorded around every kernel launch, on the stream that launch goes to) gives each launch's duration
+inside the timed region; the kernel whose launches span the most time per step is dominant, and its
+`achieved` = algorithmic bytes of the pairs one launch serves (route tally) / its mean launch duration.
+The whole chain's figure is reported beside it (`roofline.chain`).
+
+Extra legs (not timed in `value`), rank 0 at N=1: configs C4 and C5 on the same GPU (throughput, their
+own dominant kernel, an oracle parity sample), fp32 compute, warm start, the host-buffer entry, and a
+CPU baseline — the oracle restatement (kind "port") over a bounded sample of the same pairs, which also
+re-checks GPU/CPU parity on that sample.
 """
 from __future__ import annotations
 
@@ -67,6 +74,108 @@ def moved_copy(pool, delta: float, seed: int) -> np.ndarray:
     for j in range(3):
         v[idx + j * np.repeat(cnt, cnt)] += np.repeat(d[:, j], cnt)
     return v.astype(pool.verts.dtype)
+
+
+WS_COUNTERS, WS_TALLY = 32, 48          # gjkepa_kernel.h: workspace header (uint32 words)
+ROUTE_EPA0, ROUTE_CT0 = 0x10, 0x20
+
+
+def served_pairs(r, tally: np.ndarray, recs, shares: dict) -> float:
+    """Pairs one launch served: its route code's tally (workspace header, last chain), split across the
+    parts of a parted tier by the share of the batch's hits inside each part's pair range."""
+    k, code = r["kernel"].decode(), int(r["route_code"])
+    if k == "gjk" and int(r["tier"]) == 0:
+        return float(r["n_pairs"])
+    if code < 0 or code >= len(tally):
+        return 0.0
+    tot = float(tally[code])
+    key = (k, int(r["tier"]), code)
+    if key in shares and shares[key] > 0:
+        f, c = int(r["first_pair"]), int(r["n_pairs"])
+        hits = recs["collision"][f:f + c] != 0
+        return tot * float(hits.sum()) / shares[key]
+    return tot
+
+
+def dominant_kernel(lt: np.ndarray, tally: np.ndarray, recs, bpq: float, pmc: dict | None) -> dict:
+    """The kernel (kind, tier) whose launches span the most time per chain, from the launch timing of the
+    timed steps (gjkepa_launch_timing_read records)."""
+    chains = sorted(set(int(c) for c in lt["chain"]))
+    groups: dict = {}
+    for r in lt:
+        groups.setdefault((r["kernel"].decode(), int(r["tier"])), []).append(r)
+    best, best_span = None, -1.0
+    for key, rs in groups.items():
+        spans = []
+        for c in chains:
+            cr = [r for r in rs if int(r["chain"]) == c]
+            if cr:
+                spans.append(max(float(r["end_ms"]) for r in cr) - min(float(r["start_ms"]) for r in cr))
+        span = float(np.mean(spans)) if spans else 0.0
+        if span > best_span:
+            best, best_span = key, span
+    rs = groups[best]
+    # parts of one route code in several pair ranges: hits per range apportion the code's tally
+    by_code: dict = {}
+    for r in rs:
+        if int(r["chain"]) == chains[-1]:
+            by_code.setdefault((best[0], best[1], int(r["route_code"])), []).append(r)
+    shares = {}
+    for key, lst in by_code.items():
+        if len(lst) > 1:
+            shares[key] = float(sum(int((recs["collision"][int(r["first_pair"]):int(r["first_pair"]) + int(r["n_pairs"])] != 0).sum())
+                                    for r in lst))
+    last = [r for lst in by_code.values() for r in lst]
+    served = [served_pairs(r, tally, recs, shares) for r in last]
+    durs = np.array([float(r["end_ms"]) - float(r["start_ms"]) for r in rs])
+    per_chain = len(rs) / len(chains)
+    pairs_per_launch = float(np.sum(served)) / max(len(last), 1)
+    launch_ms = float(durs.mean())
+    achieved = pairs_per_launch * bpq / (launch_ms * 1e-3) / 1e9
+    span_achieved = float(np.sum(served)) * bpq / (best_span * 1e-3) / 1e9 if best_span > 0 else 0.0
+    out = {"kernel": f"{best[0]} tier {best[1]}", "launches_per_step": per_chain,
+           "pairs_per_launch": round(pairs_per_launch, 1), "pairs_per_step": float(np.sum(served)),
+           "launch_ms": round(launch_ms, 4), "launch_ms_each": [round(float(d), 4) for d in durs[-len(last):]],
+           "wall_span_ms": round(best_span, 4), "bytes_per_pair": round(bpq, 1),
+           "achieved": round(achieved, 3), "frac": round(achieved / PEAK_HBM_GBS, 6),
+           "span_achieved": round(span_achieved, 3), "span_frac": round(span_achieved / PEAK_HBM_GBS, 6),
+           "method": "HIP events around each launch (gjkepa_launch_timing) over the timed steps; pairs = the "
+                     "launch's route-code tally in the workspace (parts: split by the hits in each part's range); "
+                     "achieved = pairs per launch x bytes per pair / mean launch duration; span_* = per step, "
+                     "over the wall span from the first launch's start to the last one's end"}
+    # the same kernel in the committed PMC run (same library source hash): its traffic per launch and its
+    # VALU-busy share priced against the wall span of its launches
+    if pmc:
+        want = {"epa": "epa_kernel", "gjk": "gjk_kernel", "contact": "contact_kernel", "redo": "redo_kernel"}.get(best[0], "?")
+        cand = [(v.get("seconds", 0.0), k, v) for k, v in pmc.get("kernels", {}).items() if want in k]
+        if cand:
+            _, name, v = max(cand, key=lambda x: x[0])
+            disp = v.get("dispatches_per_chain") or 1.0
+            out["pmc"] = {"kernel": name, "traffic_per_launch": (2.0 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)) * 1024.0 / disp,
+                          "valu_instr_per_pair": v.get("SQ_INSTS_VALU", 0.0) / max(float(np.sum(served)), 1.0),
+                          "salu_per_valu": v.get("SQ_INSTS_SALU", 0.0) / max(v.get("SQ_INSTS_VALU", 1.0), 1.0),
+                          "busy_frac_span": v.get("SQ_ACTIVE_INST_VALU", 0.0) * 4.0 / (1024 * best_span * 1e-3 * 2.4e9)
+                          if best_span > 0 else None,
+                          "note": "PMC counters of the largest-time instantiation of this kernel (profiles/pmc_traffic.json), "
+                                  "summed over its dispatches per chain; busy_frac_span = SQ_ACTIVE_INST_VALU x 4 over "
+                                  "1024 SIMDs x the live wall span x 2.4 GHz"}
+    return out
+
+
+def read_tally(ws) -> np.ndarray:
+    return ws[4 * WS_COUNTERS:4 * (WS_COUNTERS + WS_TALLY)].cpu().numpy().view(np.uint32).copy()
+
+
+def pmc_entry(precision: str, config: str, n: int, lib_src: str) -> dict | None:
+    """The committed PMC summary of this (precision, config, batch) at the loaded library's source hash."""
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(prof):
+        return None
+    try:
+        pj = json.load(open(prof)).get(f"{precision}_{config}_{n}")
+    except (OSError, ValueError):
+        return None
+    return pj if pj and pj.get("src") == lib_src else None
 
 
 def host_cpus() -> dict:
@@ -176,7 +285,69 @@ def parse():
     ap.add_argument("--no-f32-leg", action="store_true", help="skip the fp32-compute side measurement")
     ap.add_argument("--no-warm-leg", action="store_true", help="skip the warm-start side measurement")
     ap.add_argument("--cpu-sample", type=int, default=0, help="pairs for the CPU baseline (0: the whole batch)")
+    ap.add_argument("--legs", default="C4,C5", help="N=1: extra configs run on the same GPU after the main one "
+                                                   "(comma list; 'none' to skip)")
+    ap.add_argument("--leg-sample", type=int, default=65536, help="pairs of each leg checked against the oracle")
+    ap.add_argument("--launch-timing", choices=["timed", "separate", "off"], default="timed",
+                    help="timed: launch events inside the timed steps; separate: in a second pass of the same steps")
     return ap.parse_args()
+
+
+def run_leg(cfg: str, args, dev, stream, prec: int, lib_src: str) -> dict:
+    """One more config on this GPU (N=1): its own batch resident in HBM, warmup, `steps` timed chains
+    with launch timing, the dominant kernel, and an oracle parity sample of its first pairs."""
+    import torch
+    nmin, nmax, rmax, n, desc = CONFIGS[cfg]
+    rec_bytes = gjkepa.load().gjkepa_record_bytes(prec)
+    pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax, dtype=np.float32)
+    verts = torch.from_numpy(pool.verts).to(dev)
+    off = torch.from_numpy(pool.hull_off).to(dev)
+    cnt = torch.from_numpy(pool.hull_cnt).to(dev)
+    prs = torch.from_numpy(pool.pairs.reshape(-1)).to(dev)
+    out = torch.zeros(n * rec_bytes, dtype=torch.uint8, device=dev)
+    ws_bytes = gjkepa.workspace_bytes_for(n, gjkepa.large_pairs(pool))
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+    sptr = stream.cuda_stream
+
+    def launch():
+        gjkepa.gjkepa_batch_device(args.version, 1.0, gjkepa.DTYPE_F32, prec, verts.data_ptr(), off.data_ptr(),
+                                   cnt.data_ptr(), prs.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws_bytes, sptr)
+    for _ in range(max(args.warmup, 1)):
+        launch()
+    torch.cuda.synchronize(dev)
+    steps = max(1, min(args.steps, 10))
+    gjkepa.launch_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        launch()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    gjkepa.launch_timing(False)
+    lt = gjkepa.launch_timing_read()
+    recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))
+    bpq = algorithmic_bytes_per_query(float(pool.hull_cnt.sum()) / n, 4, rec_bytes)
+    chain_ms = float(np.mean([lt["end_ms"][lt["chain"] == c].max() for c in set(lt["chain"].tolist())]))
+    r = {"config": cfg, "workload": f"{cfg}: {desc}", "pairs": n, "steps": steps,
+         "value": round(n * steps / el / 1e6, 3), "unit": "M queries/s", "ms_per_step": round(1e3 * el / steps, 4),
+         "chain_ms": round(chain_ms, 4), "bytes_per_query": round(bpq, 1),
+         "hit_rate": round(float((recs["collision"] != 0).mean()), 4),
+         "status_counts": {int(k): int(v) for k, v in zip(*np.unique(recs["status"], return_counts=True))},
+         "dominant_kernel": dominant_kernel(lt, read_tally(ws), recs, bpq, pmc_entry(args.precision, cfg, n, lib_src))}
+    pmc = pmc_entry(args.precision, cfg, n, lib_src)
+    if pmc:
+        r["traffic_per_chain"] = pmc["bytes_per_launch"]
+    if prec == gjkepa.PREC_F64 and args.leg_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker only, after the timed steps
+        m = min(n, args.leg_sample)
+        sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[:m])
+        ref = oracle.gjkepa_batch(sub, args.version, 1.0, host_cpus()["usable"])
+        eq = np.frombuffer(recs[:m].tobytes(), np.uint8).reshape(m, -1) == np.frombuffer(ref.tobytes(), np.uint8).reshape(m, -1)
+        r["parity_sample"] = {"pairs": m, "bitexact_records": float(eq.all(axis=1).mean()),
+                              "all_equal": bool(eq.all()), "against": "oracle, the leg's first pairs"}
+    del verts, off, cnt, prs, out, ws
+    torch.cuda.empty_cache()
+    return r
 
 
 def main():
@@ -212,7 +383,7 @@ def main():
     cnt = torch.from_numpy(pool.hull_cnt).to(dev)
     prs = torch.from_numpy(pool.pairs.reshape(-1)).to(dev)
     out = torch.zeros(n * rec_bytes, dtype=torch.uint8, device=dev)
-    ws_bytes = gjkepa.workspace_bytes(n)
+    ws_bytes = gjkepa.workspace_bytes_for(n, gjkepa.large_pairs(pool))     # park slots only where pairs can park
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
     # N > 1: every step's records are all-gathered (shard.RecordExchange); with the library's RCCL
     # communicator step i's gather overlaps step i+1's kernels (two record buffers), on gloo it is
@@ -252,6 +423,8 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    if args.launch_timing == "timed":
+        gjkepa.launch_timing(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -261,6 +434,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    timing_ms_per_step = None
+    if args.launch_timing == "separate":           # the same steps once more, with the launch events
+        gjkepa.launch_timing(True)
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        timing_ms_per_step = 1e3 * (time.perf_counter() - t1) / args.steps
+    gjkepa.launch_timing(False)
+    lt = gjkepa.launch_timing_read() if args.launch_timing != "off" else None
+    tally = read_tally(ws)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
     kern_ms_local = kern_ms
     if dist:
@@ -285,29 +470,34 @@ def main():
     # source hash; null unless that hash is the one this process loaded (no figures from another build)
     traffic, valu, pmc_src = None, None, None
     lib_src = gjkepa.source_hash()
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            pj = json.load(open(prof)).get(f"{args.precision}_{args.config}_{n}")
-            if pj and pj.get("src") == lib_src:
-                pmc_src = pj["src"]
-                traffic = pj["bytes_per_launch"]
-                if pj.get("valu_instr"):
-                    valu = {"instr_per_query": round(pj["valu_instr_per_query"], 1),
-                            "issue_frac_pmc": round(pj["valu_issue_frac"], 4),
-                            "issue_frac_live": round(pj["valu_instr"] * 2.0 / (1024 * kern_ms * 1e-3 * 2.4e9), 4),
-                            "busy_frac_pmc": round(pj["valu_busy_frac"], 4) if pj.get("valu_busy_frac") else None,
-                            "traffic_raw_fetch": pj.get("fetch_bytes_raw"),
-                            "note": "issue_frac: SQ_INSTS_VALU at the 2-cycle wave64 slot vs 1024 SIMDs x kernel time x "
-                                    "2.4 GHz (fp64 ops take 4: a lower bound); busy_frac: SQ_ACTIVE_INST_VALU (quad-cycles "
-                                    "x 4) over the same, the VALU-busy share"}
-        except Exception:
-            traffic, valu, pmc_src = None, None, None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic, "valu_issue": valu,
-                "bytes_per_query": round(bpq, 1), "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
-                "kernel": "gjk + epa + contact kernel tiers (one launch chain; HIP events on the launch stream)",
-                "pmc_src": pmc_src}
+    pj = pmc_entry(args.precision, args.config, n, lib_src)
+    if pj:
+        pmc_src = pj["src"]
+        traffic = pj["bytes_per_launch"]
+        if pj.get("valu_instr"):
+            valu = {"instr_per_query": round(pj["valu_instr_per_query"], 1),
+                    "issue_frac_pmc": round(pj["valu_issue_frac"], 4),
+                    "issue_frac_live": round(pj["valu_instr"] * 2.0 / (1024 * kern_ms * 1e-3 * 2.4e9), 4),
+                    "busy_frac_pmc": round(pj["valu_busy_frac"], 4) if pj.get("valu_busy_frac") else None,
+                    "traffic_raw_fetch": pj.get("fetch_bytes_raw"),
+                    "note": "issue_frac: SQ_INSTS_VALU at the 2-cycle wave64 slot vs 1024 SIMDs x kernel time x "
+                            "2.4 GHz (fp64 ops take 4: a lower bound); busy_frac: SQ_ACTIVE_INST_VALU (quad-cycles "
+                            "x 4) over the summed kernel time (concurrent kernels overlap: see dominant_kernel.pmc "
+                            "for the share over a wall span)"}
+    chain = {"achieved": round(achieved, 3), "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": traffic,
+             "valu_issue": valu, "bytes_per_query": round(bpq, 1), "queries_per_launch": n, "kernel_ms": round(kern_ms, 4),
+             "kernel": "gjk + epa + contact kernel tiers (one launch chain; HIP events on the launch stream)",
+             "pmc_src": pmc_src}
+    dom = dominant_kernel(lt, tally, recs, bpq, pj) if lt is not None and len(lt) else None
+    if dom is not None:
+        dom["timing"] = args.launch_timing + ("" if timing_ms_per_step is None else f" (that pass: {timing_ms_per_step:.4f} ms/step)")
+        # the dominant kernel's PMC traffic per launch (same source hash), or null
+        roofline = {"bound": "hbm", "achieved": dom["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": dom["frac"], "traffic": dom.get("pmc", {}).get("traffic_per_launch"),
+                    "kernel": dom["kernel"], "pmc_src": pmc_src, "chain": chain}
+    else:
+        roofline = {"bound": "hbm", **{k: chain[k] for k in ("achieved", "frac", "traffic", "kernel", "pmc_src")},
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "chain": chain}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "M queries/s", "n_gpus": world,
@@ -322,6 +512,7 @@ def main():
                                                        else "+gloo_allgather_host_staged"),
                    "vert_storage": "f32", "record_bytes": rec_bytes},
         "roofline": roofline,
+        "dominant_kernel": dom,
         "hit_rate": round(hit_rate, 4), "epa_iters_mean": round(epa_mean, 2), "status_counts": status_counts,
         "lib": gjkepa.version_string(),
     }
@@ -435,6 +626,13 @@ def main():
             same = (g.tobytes() == cref.tobytes())
             eq = np.frombuffer(g.tobytes(), np.uint8).reshape(m, -1) == np.frombuffer(cref.tobytes(), np.uint8).reshape(m, -1)
             result["parity_sample"] = {"pairs": m, "bitexact_records": float(eq.all(axis=1).mean()), "all_equal": bool(same)}
+
+    # configs C4 / C5 on the same GPU, after everything above (N=1 only)
+    if rank == 0 and world == 1 and args.legs.lower() != "none":
+        result["legs"] = {}
+        for cfg in [c.strip() for c in args.legs.split(",") if c.strip()]:
+            if cfg in CONFIGS and cfg != args.config:
+                result["legs"][cfg] = run_leg(cfg, args, dev, stream, prec, lib_src)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

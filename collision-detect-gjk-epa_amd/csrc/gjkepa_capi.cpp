@@ -164,6 +164,7 @@ struct Fork {
     hipEvent_t fork3 = nullptr, join3 = nullptr;
     hipStream_t s4 = nullptr;                    // contact passes of the odd parts (GJKEPA_PART_PASS_STREAMS 2)
     hipEvent_t join4 = nullptr;
+    hipEvent_t fork23 = nullptr, join23 = nullptr;   // EPA tier 3 on s3 beside tier 2 (GJKEPA_E23_STREAMS 2)
 };
 struct ForkKey {
     int dev;
@@ -201,6 +202,8 @@ int fork_state(hipStream_t s, Fork** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join3, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&f->s4, hipStreamNonBlocking, prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join4, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->fork23, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join23, hipEventDisableTiming);
     if (e != hipSuccess) {
         delete f;
         return hip_fail(e, "overlap stream / events");
@@ -316,6 +319,106 @@ static_assert(GJKEPA_ROUTE_REDO < GJKEPA_WS_TALLY && GJKEPA_ROUTE_REDO > GJKEPA_
 #ifndef GJKEPA_CONTACT_UNITS_GRID
 #define GJKEPA_CONTACT_UNITS_GRID 1
 #endif
+// EPA tiers 2 (hulls of 33-128 vertices) and 3 (129-256, first pass) serve disjoint pairs: with 2 they
+// run side by side, tier 3 on an internal stream forked after tier 1 and joined before tier 4, which
+// resumes both tiers' parked polytopes.  Tier 2's overflow then goes straight to tier 4 (a restart in
+// tier 3 would outgrow its 40-vertex polytope anyway; which tier answers never changes a record).
+// Environment override GJKEPA_E23_STREAMS for A/B.
+#ifndef GJKEPA_E23_STREAMS
+#define GJKEPA_E23_STREAMS 2
+#endif
+int e23_streams() {
+    static const int p = [] {
+        const char* e = std::getenv("GJKEPA_E23_STREAMS");
+        const int v = e ? std::atoi(e) : GJKEPA_E23_STREAMS;
+        return v == 2 ? 2 : 1;
+    }();
+    return p;
+}
+
+// Park slots.  Only EPA tiers 2 and 3 park (hulls above EPA tier 1's capacity), so the park area a
+// batch can use is sized by its pairs with a hull above kParkMinHull vertices: gjkepa_workspace_bytes_for.
+constexpr int kParkMinHull = epa_hull_cap(1);
+static_assert(epa_hull_cap(0) <= kParkMinHull, "EPA tiers 0 and 1 never park");
+int64_t ws_bytes_for(int64_t n_pairs, int64_t n_large) {
+    return ws_base(n_pairs) + (n_large + kParkShare - 1) / kParkShare * GJKEPA_PARK_BYTES;
+}
+// pairs of a host-side pair list with a hull above kParkMinHull vertices
+int64_t count_large(const int32_t* pairs, int64_t n_pairs, const int32_t* hull_cnt) {
+    int64_t n = 0;
+    for (int64_t k = 0; k < n_pairs; ++k)
+        n += hull_cnt[pairs[2 * k]] > kParkMinHull || hull_cnt[pairs[2 * k + 1]] > kParkMinHull;
+    return n;
+}
+
+// ---- per-launch timing (gjkepa_launch_timing; bench.py's dominant-kernel roofline) -------------------
+// With timing on for the calling thread, each chain it enqueues records one event at its head on the
+// caller's stream and two around every kernel launch, on the stream that launch goes to.
+// gjkepa_launch_timing_read waits for them and reports each launch's start / end relative to its
+// chain's head.  Timing events are barrier markers in the stream's queue; a launch's start is when the
+// stream reached it (its previous work on that stream had finished).
+struct TimedLaunch {
+    gjkepa_launch_time info;
+    hipEvent_t head, b, e;
+};
+struct Timing {
+    bool on = false;
+    int chain = -1;
+    hipEvent_t head = nullptr;
+    std::vector<hipStream_t> streams;        // this chain's streams, in order of first use (0: caller's)
+    std::vector<TimedLaunch> launches;
+    std::vector<hipEvent_t> pool;            // events no pending launch refers to
+    std::vector<hipEvent_t> used;
+    hipEvent_t get() {
+        hipEvent_t ev = nullptr;
+        if (!pool.empty()) {
+            ev = pool.back();
+            pool.pop_back();
+        } else if (hipEventCreate(&ev) != hipSuccess) {
+            return nullptr;
+        }
+        used.push_back(ev);
+        return ev;
+    }
+};
+constexpr size_t kTimingMax = 1 << 16;       // launches kept between two reads
+static_assert(sizeof(gjkepa_launch_time) == 64, "gjkepa_launch_time layout (gjkepa.py LAUNCH_TIME)");
+thread_local Timing g_tm;
+
+// start a chain on caller stream s (no-op unless timing is on)
+void timing_chain(hipStream_t s) {
+    if (!g_tm.on || g_tm.launches.size() >= kTimingMax) return;
+    g_tm.head = g_tm.get();
+    if (!g_tm.head || hipEventRecord(g_tm.head, s) != hipSuccess) { g_tm.head = nullptr; return; }
+    ++g_tm.chain;
+    g_tm.streams.assign(1, s);
+}
+// launch f() on stream st, bracketed by timing events when on
+template <typename F>
+hipError_t timed(const char* kind, int tier, int part, int route_code, int64_t first, int64_t count, hipStream_t st,
+                 F&& f) {
+    if (!g_tm.on || !g_tm.head || g_tm.launches.size() >= kTimingMax) return f();
+    TimedLaunch t{};
+    std::snprintf(t.info.kernel, sizeof(t.info.kernel), "%s", kind);
+    t.info.tier = tier;
+    t.info.part = part;
+    t.info.route_code = route_code;
+    t.info.chain = g_tm.chain;
+    int sid = 0;
+    while (sid < (int)g_tm.streams.size() && g_tm.streams[(size_t)sid] != st) ++sid;
+    if (sid == (int)g_tm.streams.size()) g_tm.streams.push_back(st);
+    t.info.stream = sid;
+    t.info.first_pair = first;
+    t.info.n_pairs = count;
+    t.head = g_tm.head;
+    t.b = g_tm.get();
+    t.e = g_tm.get();
+    if (t.b) (void)hipEventRecord(t.b, st);
+    const hipError_t e = f();
+    if (t.e) (void)hipEventRecord(t.e, st);
+    if (e == hipSuccess && t.b && t.e) g_tm.launches.push_back(t);
+    return e;
+}
 
 int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision, const void* verts,
             const int64_t* hull_off, const int32_t* hull_cnt, const int32_t* pairs, int64_t n_pairs,
@@ -329,6 +432,7 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     uint8_t* route = (uint8_t*)workspace + kWsHeader;
     const int64_t park_slots = ws_bytes > ws_base(n_pairs) ? (ws_bytes - ws_base(n_pairs)) / GJKEPA_PARK_BYTES : 0;
     hipError_t e;
+    timing_chain(s);
     if (!warm && n_pairs <= kFusedMax) {                 // small batch: one launch, one wave per pair
         gjkepa_epa_args q{};
         q.version = version;
@@ -341,13 +445,15 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         q.out = out;
         q.num_cus = num_cus;
         q.guard = gjkepa_guard_of(q);
-        if ((e = gjkepa_launch_query(vert_dtype, precision, q, s)) != hipSuccess) return hip_fail(e, "query kernel launch");
+        if ((e = timed("query", 0, 0, -1, 0, n_pairs, s, [&] { return gjkepa_launch_query(vert_dtype, precision, q, s); })) !=
+            hipSuccess)
+            return hip_fail(e, "query kernel launch");
         return 0;
     }
     static_assert(sizeof(uint32_t) * (kWsParkWord + 1) <= kWsHeader, "workspace header");
     // counter / tally / park counter reset: a one-wave kernel rather than a memset, so a captured
     // chain is kernel nodes only
-    if ((e = gjkepa_launch_ws_reset(ctr, kWsParkWord + 1, s)) != hipSuccess)
+    if ((e = timed("reset", 0, 0, -1, 0, 0, s, [&] { return gjkepa_launch_ws_reset(ctr, kWsParkWord + 1, s); })) != hipSuccess)
         return hip_fail(e, "workspace counter reset");
     uint32_t* tally = ctr + GJKEPA_WS_COUNTERS;
     int launch = 0;
@@ -366,12 +472,16 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     g.ctr = ctr + launch++;
     g.claim = 1;
     g.guard = gjkepa_guard_of(g);
-    if ((e = gjkepa_launch_gjk(0, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 0 launch");
+    if ((e = timed("gjk", 0, 0, -1, 0, n_pairs, s, [&] { return gjkepa_launch_gjk(0, vert_dtype, precision, g, s); })) !=
+        hipSuccess)
+        return hip_fail(e, "GJK tier 0 launch");
     g.route_code = GJKEPA_ROUTE_GJK1;                    // GJK tier 1: hulls above tier 0's capacity
     g.ctr = ctr + launch++;
     g.claim = kSparseClaim;
     g.guard = gjkepa_guard_of(g);
-    if ((e = gjkepa_launch_gjk(1, vert_dtype, precision, g, s)) != hipSuccess) return hip_fail(e, "GJK tier 1 launch");
+    if ((e = timed("gjk", 1, 0, g.route_code, 0, n_pairs, s, [&] { return gjkepa_launch_gjk(1, vert_dtype, precision, g, s); })) !=
+        hipSuccess)
+        return hip_fail(e, "GJK tier 1 launch");
     gjkepa_epa_args a{};
     a.version = version;
     a.tol_ff = tol_ff;
@@ -393,16 +503,20 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     int rc;
     if (GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin && (rc = fork_state(s, &f))) return rc;
     const bool overlap = f != nullptr;
+    const bool e23 = overlap && e23_streams() == 2;      // EPA tiers 2 and 3 side by side
     const gjkepa_epa_args whole = a;                     // (a.pairs / route / out / n_pairs: a pair range below)
+    int64_t r_first = 0;                                 // the pair range `a` points at
     auto range = [&](int64_t first, int64_t count) {     // point `a` at pairs [first, first + count)
         a.pairs = whole.pairs + 2 * first;
         a.route = whole.route + first;
         a.out = (unsigned char*)whole.out + first * (precision == GJKEPA_PREC_F64 ? 128 : 64);
         a.n_pairs = count;
+        r_first = first;
     };
-    auto epa_tier = [&](int t) -> int {                  // EPA tier t; polytope overflow -> t+1
+    auto epa_tier = [&](int t, hipStream_t es) -> int {  // EPA tier t on stream es; polytope overflow -> next
         a.route_code = GJKEPA_ROUTE_EPA0 + t;
-        a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + 1;
+        // beside tier 3, tier 2's overflow goes to tier 4 (tier 3 is running: its tally is final at its start)
+        a.next_code = t == GJKEPA_EPA_TIERS - 1 ? -1 : GJKEPA_ROUTE_EPA0 + t + (e23 && t == 2 ? 2 : 1);
         a.ct_base = overlap ? GJKEPA_ROUTE_CT(fork_point(t)) : GJKEPA_ROUTE_CT0;
         a.ctr = ctr + launch++;
         a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
@@ -411,20 +525,24 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         // when the tier is empty (C5: an empty launch spanned 1.1 ms of the chain)
         a.grid = t == GJKEPA_EPA_TIERS - 1 ? num_cus : 0;
         a.guard = gjkepa_guard_of(a);
-        hipError_t er = gjkepa_launch_epa(t, vert_dtype, precision, a, s);
+        hipError_t er = timed("epa", t, 0, a.route_code, r_first, a.n_pairs, es,
+                              [&] { return gjkepa_launch_epa(t, vert_dtype, precision, a, es); });
         return er == hipSuccess ? 0 : hip_fail(er, "EPA tier launch");
     };
-    // contact features of the EPA results under route codes base + contact tier (tiers 0..ntiers-1)
-    auto contact_tiers = [&](int base, int ntiers, hipStream_t cs) -> int {
+    // contact features of the EPA results under route codes base + contact tier (tiers 0..ntiers-1).
+    // `single`: every launch claims single chunks.  A pass forked after one part of a parted tier must:
+    // the other parts are still adding to the route tally its sparse/dense choice (pick_claim) reads.
+    auto contact_tiers = [&](int base, int ntiers, hipStream_t cs, bool single, int part) -> int {
         for (int t = 0; t < ntiers; ++t) {
             a.route_code = base + t;
             a.next_code = -1;
             a.ctr = ctr + launch++;
-            a.claim = (t == 0 && base <= GJKEPA_ROUTE_CT(0)) ? 1 : kSparseClaim;
+            a.claim = (single || (t == 0 && base <= GJKEPA_ROUTE_CT(0))) ? 1 : kSparseClaim;
             // a forked dense pass (EPA tier 0's hits) takes one workgroup per chunk
             a.grid = GJKEPA_CONTACT_UNITS_GRID && cs != s && a.claim == 1 ? GJKEPA_GRID_UNITS : 0;
             a.guard = gjkepa_guard_of(a);
-            hipError_t er = gjkepa_launch_contact(t, vert_dtype, precision, a, cs);
+            hipError_t er = timed("contact", t, part, a.route_code, r_first, a.n_pairs, cs,
+                                  [&] { return gjkepa_launch_contact(t, vert_dtype, precision, a, cs); });
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
         }
         return 0;
@@ -439,7 +557,8 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         a.claim = kSparseClaim;
         a.grid = 0;
         a.guard = gjkepa_guard_of(a);
-        hipError_t er = gjkepa_launch_redo(vert_dtype, a, s);
+        hipError_t er = timed("redo", 0, 0, a.route_code, r_first, a.n_pairs, s,
+                              [&] { return gjkepa_launch_redo(vert_dtype, a, s); });
         return er == hipSuccess ? 0 : hip_fail(er, "fp32 redo launch");
     };
     if (overlap) {
@@ -472,36 +591,50 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
                 a.claim = t < GJKEPA_DENSE_EPA_TIERS ? 1 : kSparseClaim;
                 a.grid = 0;
                 a.guard = gjkepa_guard_of(a);
-                if ((e = gjkepa_launch_epa(t, vert_dtype, precision, a, ps)) != hipSuccess) return hip_fail(e, "EPA tier launch");
+                if ((e = timed("epa", t, i, a.route_code, first, count, ps,
+                               [&] { return gjkepa_launch_epa(t, vert_dtype, precision, a, ps); })) != hipSuccess)
+                    return hip_fail(e, "EPA tier launch");
                 hipEvent_t pe = f->part[(t == 0 ? 0 : kPartsMax) + i];
                 hipStream_t cs = part_pass_streams() == 2 && (i & 1) ? f->s4 : f->s2[t];
                 if ((e = hipEventRecord(pe, ps)) != hipSuccess || (e = hipStreamWaitEvent(cs, pe, 0)) != hipSuccess)
                     return hip_fail(e, "contact pass fork");
-                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), cs))) return rc;
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), cs, true, i))) return rc;
                 if (cs == f->s4) used4 = true;
             }
             if (two && ((e = hipEventRecord(f->join3, f->s3)) != hipSuccess || (e = hipStreamWaitEvent(s, f->join3, 0)) != hipSuccess))
                 return hip_fail(e, "EPA part stream join");
             a = whole;
+            r_first = 0;
             forked[t] = true;
             return 0;
         };
         for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {
             const bool forks = ((GJKEPA_FORK_MASK >> t) & 1) && !(GJKEPA_LAST_PASS_MAIN && t == last);
-            const int np = !forks ? 1 : t == 0 ? epa0_parts() : t == 2 ? epa2_parts() : 1;
+            if (e23 && t == 2) {
+                // tier 3 on s3, forked here (after tier 1) and joined below before tier 4
+                if ((e = hipEventRecord(f->fork23, s)) != hipSuccess || (e = hipStreamWaitEvent(f->s3, f->fork23, 0)) != hipSuccess)
+                    return hip_fail(e, "EPA tier 3 stream fork");
+                if ((rc = epa_tier(3, f->s3))) return rc;
+                if ((e = hipEventRecord(f->join23, f->s3)) != hipSuccess) return hip_fail(e, "EPA tier 3 stream join");
+                static_assert(!((GJKEPA_FORK_MASK >> 3) & 1), "no contact pass is forked after EPA tier 3");
+            }
+            if (e23 && t == 3) continue;                     // launched beside tier 2
+            if (e23 && t == 4 && (e = hipStreamWaitEvent(s, f->join23, 0)) != hipSuccess)
+                return hip_fail(e, "EPA tier 3 stream join");
+            const int np = !forks ? 1 : t == 0 ? epa0_parts() : t == 2 && !e23 ? epa2_parts() : 1;
             if (np > 1) {
                 if ((rc = parted(t, np))) return rc;
                 continue;
             }
-            if ((rc = epa_tier(t))) return rc;
+            if ((rc = epa_tier(t, s))) return rc;
             if (!((GJKEPA_FORK_MASK >> t) & 1)) continue;
             if (GJKEPA_LAST_PASS_MAIN && t == last) {
-                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), s))) return rc;
+                if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), s, false, 0))) return rc;
                 continue;
             }
             if ((e = hipEventRecord(f->fork[t], s)) != hipSuccess || (e = hipStreamWaitEvent(f->s2[t], f->fork[t], 0)) != hipSuccess)
                 return hip_fail(e, "contact pass fork");
-            if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), f->s2[t]))) return rc;
+            if ((rc = contact_tiers(GJKEPA_ROUTE_CT(t), fork_contact_tiers(t), f->s2[t], false, 0))) return rc;
             forked[t] = true;
         }
         for (int t = 0; t < GJKEPA_EPA_TIERS; ++t) {      // join every internal stream used (last one per stream)
@@ -517,8 +650,8 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
         return redo();
     }
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
-        if ((rc = epa_tier(t))) return rc;
-    if ((rc = contact_tiers(GJKEPA_ROUTE_CT0, GJKEPA_CONTACT_TIERS, s))) return rc;
+        if ((rc = epa_tier(t, s))) return rc;
+    if ((rc = contact_tiers(GJKEPA_ROUTE_CT0, GJKEPA_CONTACT_TIERS, s, false, 0))) return rc;
     return redo();
 }
 
@@ -556,7 +689,43 @@ int gjkepa_record_bytes(int32_t precision) {
 
 int64_t gjkepa_workspace_bytes(int64_t n_pairs) {
     if (n_pairs < 0) return GJKEPA_E_ARG;
-    return ws_base(n_pairs) + (n_pairs + kParkShare - 1) / kParkShare * GJKEPA_PARK_BYTES;
+    return ws_bytes_for(n_pairs, n_pairs);
+}
+
+int64_t gjkepa_workspace_bytes_for(int64_t n_pairs, int64_t n_large_pairs) {
+    if (n_pairs < 0 || n_large_pairs < 0 || n_large_pairs > n_pairs) return GJKEPA_E_ARG;
+    return ws_bytes_for(n_pairs, n_large_pairs);
+}
+
+int gjkepa_launch_timing(int32_t enable) {
+    const int prev = g_tm.on ? 1 : 0;
+    g_tm.on = enable != 0;
+    return prev;
+}
+
+int gjkepa_launch_timing_read(gjkepa_launch_time* out, int32_t max) {
+    if (max < 0 || (max > 0 && !out)) return fail(GJKEPA_E_ARG, "bad timing buffer");
+    int n = 0;
+    hipError_t e = hipSuccess;
+    for (const TimedLaunch& t : g_tm.launches) {
+        if ((e = hipEventSynchronize(t.e)) != hipSuccess) break;
+        if (n >= max) continue;
+        out[n] = t.info;
+        float a = 0.f, b = 0.f;
+        if ((e = hipEventElapsedTime(&a, t.head, t.b)) != hipSuccess || (e = hipEventElapsedTime(&b, t.head, t.e)) != hipSuccess)
+            break;
+        out[n].start_ms = a;
+        out[n].end_ms = b;
+        ++n;
+    }
+    // every event of the read launches is free again (an unread tail is dropped with them)
+    for (hipEvent_t ev : g_tm.used) (void)hipEventSynchronize(ev);
+    g_tm.pool.insert(g_tm.pool.end(), g_tm.used.begin(), g_tm.used.end());
+    g_tm.used.clear();
+    g_tm.launches.clear();
+    g_tm.head = nullptr;
+    g_tm.chain = -1;
+    return e == hipSuccess ? n : hip_fail(e, "launch timing events");
 }
 
 const char* gjkepa_last_error(void) { return g_err.c_str(); }
@@ -627,6 +796,8 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
         if (c >= 1 && (hull_off[h] < 0 || hull_off[h] + 3 * c > n_vert_scalars))
             return fail(GJKEPA_E_ARG, "hull outside the vertex pool");
     }
+    // park slots only for the pairs that can reach the parking EPA tiers
+    const int64_t wsb = ws_bytes_for(n_pairs, count_large(pairs, n_pairs, hull_cnt));
     int rc = 0;
     DeviceState* d = device_state(device, &rc);
     if (!d) return rc;
@@ -640,7 +811,7 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
         (e = d->cnt.ensure((size_t)n_hulls * 4)) != hipSuccess ||
         (e = d->pairs.ensure((size_t)n_pairs * 8)) != hipSuccess ||
         (e = d->out.ensure((size_t)n_pairs * rec)) != hipSuccess ||
-        (e = d->ws.ensure((size_t)gjkepa_workspace_bytes(n_pairs))) != hipSuccess)
+        (e = d->ws.ensure((size_t)wsb)) != hipSuccess)
         return hip_fail(e, "hipMalloc");
     hipStream_t s = d->stream;
     if ((e = hipMemcpyAsync(d->verts.p, verts, (size_t)n_vert_scalars * esz, hipMemcpyHostToDevice, s)) != hipSuccess ||
@@ -717,6 +888,8 @@ int run_queries_on(DeviceState* d, std::vector<Query*>& qs, int device) {
     if (nq == 0) return 0;
     size_t nv = 0;
     for (Query* q : qs) nv += 3 * (size_t)(q->n1 + q->n2);
+    int64_t nlarge = 0;                       // pairs that can park (ws_bytes_for)
+    for (Query* q : qs) nlarge += q->n1 > kParkMinHull || q->n2 > kParkMinHull;
     const size_t rec = sizeof(gjkepa_contact_f64);
     const size_t o_v = nq * rec, o_off = o_v + 8 * (nv + 1), o_cnt = o_off + 8 * 2 * nq;
     const size_t o_pr = o_cnt + 4 * 2 * nq, total = o_pr + 4 * 2 * nq;
@@ -725,7 +898,7 @@ int run_queries_on(DeviceState* d, std::vector<Query*>& qs, int device) {
     if (rc) return rc;
     hipError_t e;
     if ((e = d->q_host.ensure(total)) != hipSuccess || (e = d->q_blk.ensure(total)) != hipSuccess ||
-        (e = d->q_ws.ensure((size_t)gjkepa_workspace_bytes((int64_t)nq))) != hipSuccess)
+        (e = d->q_ws.ensure((size_t)ws_bytes_for((int64_t)nq, nlarge))) != hipSuccess)
         return hip_fail(e, "query staging allocation");
     char* h = (char*)d->q_host.p;
     double* v = (double*)(h + o_v);
@@ -806,7 +979,26 @@ struct Service {
     // steps of kSvcGridStep; a caller whose slot has no wave stops the grid and relaunches it larger.
     std::atomic<int> grid_n{0};
     std::atomic<int> hi{0};                   // highest slot + 1 claimed since the last launch
+    // slots whose request a failed call left unanswered (a late wave could still read them): held out
+    // of use until no grid runs, then marked answered and freed (release_stuck)
+    std::atomic<uint64_t> stuck{0};
 };
+// a grid answering `slot` is not wanted: the service was turned off (gjkepa_query_service_set(0)) while
+// the call was in flight; the caller goes through the combining path instead
+constexpr int kSvcOff = 1;
+
+// no grid is running (the caller holds sv->mu and has waited for the latest one): every stuck slot's
+// request is marked answered, so a later wave (which starts from `done`) never reads it, and the slot
+// is free again
+void release_stuck(Service* sv) {
+    uint64_t m = sv->stuck.exchange(0, std::memory_order_acq_rel);
+    while (m) {
+        const int k = __builtin_ctzll(m);
+        m &= m - 1;
+        __atomic_store_n(&sv->slots[k].done, __atomic_load_n(&sv->slots[k].req, __ATOMIC_ACQUIRE), __ATOMIC_RELEASE);
+        sv->free_slots.fetch_or(1ull << k, std::memory_order_release);
+    }
+}
 constexpr int kSvcGridStep = 8;
 static_assert(GJKEPA_SVC_SLOTS >= 1 && GJKEPA_SVC_SLOTS <= 64, "service slot bitmap");
 std::mutex g_svc_mu;
@@ -921,6 +1113,10 @@ int service_ensure(Service* sv, bool check_done, int slot) {
         if (small) for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 0u, __ATOMIC_RELEASE);
         if (e != hipSuccess) return hip_fail(e, "query service drain");
     }
+    release_stuck(sv);                        // no grid runs here
+    // turned off (gjkepa_query_service_set(0)) while a call was in flight: no relaunch; the grid has
+    // drained, so the caller's slot is no longer read and it combines instead
+    if (!service_enabled()) return kSvcOff;
     if ((e = hipSetDevice(sv->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
     uint32_t ng = g1 + 1;
     if (ng == 0) ng = 1;
@@ -980,7 +1176,15 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
     if (seq == 0) seq = 1;
     sv->seq[k] = seq;
     __atomic_store_n(&sl->req, seq, __ATOMIC_RELEASE);
+    // kSvcOff: no grid runs and none will be launched; an unanswered request is marked answered (the
+    // slot's next wave starts from `done`), an answered one is returned as usual
+    auto off = [&]() -> int {
+        if (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) == seq) return 0;
+        __atomic_store_n(&sl->done, seq, __ATOMIC_RELEASE);
+        return kSvcOff;
+    };
     int rc = service_ensure(sv, false, k);
+    if (rc == kSvcOff && (rc = off()) != 0) return rc;
     if (rc) return rc;
     const auto t0 = std::chrono::steady_clock::now();
     auto next_check = t0 + std::chrono::microseconds(200);
@@ -994,9 +1198,15 @@ int service_run(Service* sv, int k, int32_t version, double tol_ff, const double
             const auto now = std::chrono::steady_clock::now();
             yield = now - t0 > std::chrono::microseconds(80);
             // a grid that reached its idle or lifetime limit marks itself closing: relaunch at once
-            if ((rc = service_ensure(sv, false, k)) != 0) return rc;
+            if ((rc = service_ensure(sv, false, k)) != 0) {
+                if (rc == kSvcOff && (rc = off()) == 0) break;
+                return rc;
+            }
             if (now >= next_check) {              // the grid may have drained under this request
-                if ((rc = service_ensure(sv, true, k)) != 0) return rc;
+                if ((rc = service_ensure(sv, true, k)) != 0) {
+                    if (rc == kSvcOff && (rc = off()) == 0) break;
+                    return rc;
+                }
                 next_check = now + std::chrono::microseconds(200);
                 if (now - t0 > std::chrono::seconds(30)) return fail(GJKEPA_E_HIP, "query service: no answer in 30 s");
             }
@@ -1028,15 +1238,21 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     Service* sv = service_enabled() && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS &&
                   device >= 0 && device < device_count_cached() ? service(device) : nullptr;
     const int slot = sv ? service_claim(sv) : -1;
-    if (slot < 0 && !device_state(device, &rc)) return rc;
+    bool served = false;
     if (slot >= 0) {
         rc = service_run(sv, slot, version, tol_ff, p1, n1, p2, n2, &me.rec);
         // a request that may still be read by a late wave (no answer, or no grid launched) keeps its
-        // slot: the next holder would overwrite the hulls under that wave
-        if (rc == 0 || __atomic_load_n(&sv->slots[slot].done, __ATOMIC_ACQUIRE) == sv->seq[slot])
+        // slot out of use until no grid runs (release_stuck): the next holder would overwrite the hulls
+        // under that wave
+        if (rc == 0 || rc == kSvcOff || __atomic_load_n(&sv->slots[slot].done, __ATOMIC_ACQUIRE) == sv->seq[slot])
             sv->free_slots.fetch_or(1ull << slot, std::memory_order_release);
-        if (rc) return rc;
-    } else {
+        else
+            sv->stuck.fetch_or(1ull << slot, std::memory_order_release);
+        if (rc != 0 && rc != kSvcOff) return rc;
+        served = rc == 0;
+    }
+    if (!served && !device_state(device, &rc)) return rc;
+    if (!served) {
     Combiner* cb = combiner(device);
     {
         std::unique_lock<std::mutex> lk(cb->mu);
@@ -1107,6 +1323,7 @@ int gjkepa_query_service_stop(int32_t device) {
         // every wave answers the request its slot holds, sees its stop word and leaves
         const hipError_t e = hipEventSynchronize(sv->ev);
         for (int k = 0; k < GJKEPA_SVC_SLOTS; ++k) __atomic_store_n(&sv->slots[k].stop, 0u, __ATOMIC_RELEASE);
+        if (e == hipSuccess) release_stuck(sv);
         __atomic_store_n(sv->closing, gen, __ATOMIC_RELEASE);   // the next call relaunches
         if (e != hipSuccess) return hip_fail(e, "query service stop");
     }
@@ -1383,7 +1600,11 @@ int gjkepa_collide(int32_t version, double tol_ff, int32_t vert_dtype, int32_t p
     if (n_candidates) *n_candidates = ncand;
     if (ncand == 0) return 0;
     // narrow phase on the device-resident list, then the dense hit list
-    const int64_t wsn = gjkepa_workspace_bytes(ncand), wsc = gjkepa_compact_ws_bytes(ncand);
+    // park slots: the candidates can only reach the parking EPA tiers when some hull is above their
+    // capacity (the pairs are on the device; the share is taken over every candidate then)
+    bool large = false;
+    for (int64_t h = 0; h < n_hulls && !large; ++h) large = hull_cnt[h] > kParkMinHull;
+    const int64_t wsn = ws_bytes_for(ncand, large ? ncand : 0), wsc = gjkepa_compact_ws_bytes(ncand);
     if (wsc < 0) return fail(GJKEPA_E_HIP, "compaction workspace query failed");
     if ((e = d->out.ensure((size_t)ncand * rec)) != hipSuccess || (e = d->ws.ensure((size_t)wsn)) != hipSuccess ||
         (e = d->c_idx.ensure((size_t)ncand * 4)) != hipSuccess || (e = d->c_hits.ensure((size_t)ncand * rec)) != hipSuccess ||

@@ -35,7 +35,8 @@ EXPORTS = (
     "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
     "gjkepa_collide", "gjkepa_shard_range", "gjkepa_batch_multi", "gjkepa_comm_unique_id", "gjkepa_comm_init",
     "gjkepa_comm_destroy", "gjkepa_comm_backend", "gjkepa_allgather_records_device",
-    "gjkepa_query_service_stop", "gjkepa_query_service_set",
+    "gjkepa_query_service_stop", "gjkepa_query_service_set", "gjkepa_workspace_bytes_for",
+    "gjkepa_launch_timing", "gjkepa_launch_timing_read",
 )
 COMM_ID_BYTES = 128
 # workspace header word counting the park slots a gjkepa_batch_device call took (diagnostics; csrc/
@@ -144,6 +145,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_query_service_stop.restype = ctypes.c_int
     lib.gjkepa_query_service_set.argtypes = [c_i32]
     lib.gjkepa_query_service_set.restype = ctypes.c_int
+    lib.gjkepa_workspace_bytes_for.argtypes = [c_i64, c_i64]
+    lib.gjkepa_workspace_bytes_for.restype = c_i64
+    lib.gjkepa_launch_timing.argtypes = [c_i32]
+    lib.gjkepa_launch_timing.restype = ctypes.c_int
+    lib.gjkepa_launch_timing_read.argtypes = [c_vp, c_i32]
+    lib.gjkepa_launch_timing_read.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -278,6 +285,47 @@ def gjkepa_batch(pool: HullPool, version: int = 2, tol_ff: float = 1.0, precisio
 
 def workspace_bytes(n_pairs: int) -> int:
     return int(load().gjkepa_workspace_bytes(n_pairs))
+
+
+PARK_MIN_HULL = 32   # pairs with a hull above this many vertices can reach the parking EPA tiers
+
+
+def large_pairs(pool: HullPool) -> int:
+    """Pairs of the pool with a hull above PARK_MIN_HULL vertices (gjkepa_workspace_bytes_for)."""
+    c = pool.hull_cnt[pool.pairs.astype(np.int64)]
+    return int((c.max(axis=1) > PARK_MIN_HULL).sum()) if pool.n_pairs else 0
+
+
+def workspace_bytes_for(n_pairs: int, n_large_pairs: int) -> int:
+    """Workspace with park slots only for the pairs that can park (include/gjkepa.h)."""
+    b = int(load().gjkepa_workspace_bytes_for(int(n_pairs), int(n_large_pairs)))
+    if b < 0:
+        raise GjkEpaError("gjkepa_workspace_bytes_for: bad arguments")
+    return b
+
+
+# per-launch timing of the tier chain (include/gjkepa.h gjkepa_launch_time)
+LAUNCH_TIME = np.dtype([
+    ("kernel", "S16"), ("tier", "<i4"), ("part", "<i4"), ("route_code", "<i4"), ("chain", "<i4"),
+    ("stream", "<i4"), ("pad", "<i4"), ("first_pair", "<i8"), ("n_pairs", "<i8"), ("start_ms", "<f4"),
+    ("end_ms", "<f4"),
+])
+assert LAUNCH_TIME.itemsize == 64
+
+
+def launch_timing(enable: bool) -> bool:
+    """Record HIP events around every kernel launch of the chains this thread enqueues from now on;
+    returns the previous setting."""
+    return bool(load().gjkepa_launch_timing(1 if enable else 0))
+
+
+def launch_timing_read(max_launches: int = 1 << 16) -> np.ndarray:
+    """Wait for the recorded launches and return them (LAUNCH_TIME records, enqueue order)."""
+    buf = np.zeros(max_launches, LAUNCH_TIME)
+    n = load().gjkepa_launch_timing_read(_ptr(buf), max_launches)
+    if n < 0:
+        _check(n, "gjkepa_launch_timing_read")
+    return buf[:n]
 
 
 def gjkepa_batch_device(version: int, tol_ff: float, vert_dtype: int, precision: int, verts_ptr: int,

@@ -157,6 +157,33 @@ int gjkepa_batch(int32_t version, double tol_ff, int32_t vert_dtype, int32_t pre
  * the route bytes rounded up to 256; park slots are used as far as the workspace provides them.  It
  * may be reused between calls on the same stream. */
 int64_t gjkepa_workspace_bytes(int64_t n_pairs);
+/* The same with park slots for one in 8 of `n_large_pairs`: the pairs with a hull above 32 vertices,
+ * the only ones that can reach the parking EPA tiers (0 for a batch of small hulls such as config C2:
+ * header and route bytes only).  gjkepa_workspace_bytes(n) = gjkepa_workspace_bytes_for(n, n). */
+int64_t gjkepa_workspace_bytes_for(int64_t n_pairs, int64_t n_large_pairs);
+
+/* ---- per-launch timing (diagnostics; bench.py's dominant-kernel roofline) ---------------------
+ * gjkepa_launch_timing(1): every later chain the calling thread enqueues (gjkepa_batch_device and the
+ * entries built on it) records a timing event at its head on the caller's stream and one before and
+ * after each kernel launch, on the stream that launch goes to (the caller's or an internal one).
+ * gjkepa_launch_timing_read waits for those events and writes up to `max` entries, one per launch in
+ * enqueue order; it returns the number written and forgets every recorded launch.  Returns the
+ * previous setting / a GJKEPA_E_* code.  Not for graph capture. */
+typedef struct gjkepa_launch_time {
+    char     kernel[16];    /* "reset", "gjk", "epa", "contact", "redo" or "query" */
+    int32_t  tier;          /* kernel tier (contact tier for "contact") */
+    int32_t  part;          /* part index of a tier launched over consecutive pair ranges, else 0 */
+    int32_t  route_code;    /* the pairs it serves (-1: every pair) */
+    int32_t  chain;         /* enqueue call, counted from 0 since the last read */
+    int32_t  stream;        /* 0: the caller's stream; 1..: the chain's internal streams, by first use */
+    int32_t  pad;
+    int64_t  first_pair;    /* pair range the launch scans */
+    int64_t  n_pairs;
+    float    start_ms;      /* events before / after the launch, ms after the chain's head event */
+    float    end_ms;
+} gjkepa_launch_time;
+int gjkepa_launch_timing(int32_t enable);
+int gjkepa_launch_timing_read(gjkepa_launch_time* out, int32_t max);
 int gjkepa_batch_device(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precision,
                         const void* verts, const int64_t* hull_off, const int32_t* hull_cnt,
                         const int32_t* pairs, int64_t n_pairs,

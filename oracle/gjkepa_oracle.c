@@ -351,7 +351,7 @@ int oracle_epa_trace = 0;
 /* fp32 certificate thresholds (ORC_F32 only; see gjkepa_kernel.hip "fp32 certificate"): the largest
  * drop of the polytope's MINLOC distance between iterations, and the largest support gap
  * h_M(n) - depth at termination, both relative to max(1, depth). */
-double oracle_cert_drop = 1e-5, oracle_cert_gap = 1e-5, oracle_cert_touch = 1e-5;
+double oracle_cert_drop = 5e-7, oracle_cert_gap = 5e-7, oracle_cert_touch = 1e-5;
 static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: touch / outside */
 static _Thread_local double g_cert_scale;   /* max |coordinate| of A + that of B */
 #include <stdio.h>

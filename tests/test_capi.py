@@ -51,6 +51,26 @@ def test_workspace_bytes(lib):
     assert lib.gjkepa_workspace_bytes(-1) < 0
 
 
+def test_workspace_bytes_for(lib):
+    """Park slots (2880 B) for one in 8 of the pairs that can park; none for a batch of small hulls."""
+    base = (512 + 100000 + 255) // 256 * 256
+    assert gjkepa.workspace_bytes_for(100000, 0) == base
+    assert gjkepa.workspace_bytes_for(100000, 100000) == gjkepa.workspace_bytes(100000) == base + 12500 * 2880
+    assert gjkepa.workspace_bytes_for(100000, 9) == base + 2 * 2880
+    assert lib.gjkepa_workspace_bytes_for(10, 11) < 0 and lib.gjkepa_workspace_bytes_for(-1, 0) < 0
+    pool = gjkepa.HullPool(np.zeros(0, np.float32), np.zeros(4, np.int64), np.array([8, 32, 33, 256], np.int32),
+                           np.array([[0, 1], [1, 2], [3, 0], [1, 1]], np.int32))
+    assert gjkepa.large_pairs(pool) == 2
+
+
+def test_launch_timing_api_without_gpu(lib):
+    """Timing on/off and an empty read need no device."""
+    assert gjkepa.launch_timing(True) is False
+    assert gjkepa.launch_timing(False) is True
+    assert len(gjkepa.launch_timing_read()) == 0
+    assert lib.gjkepa_launch_timing_read(None, -1) < 0
+
+
 def test_argument_validation_without_gpu(lib):
     # invalid enums / null pointers are rejected before any device work
     assert lib.gjkepa_batch(2, 1.0, 7, 1, None, 0, None, None, 0, None, 1, None, 0) == -1

@@ -8,7 +8,19 @@
   shard / hull-range rebase / per-shard thread path, and the shards of one device run in turn.
 - The library's RCCL communicator (world 1 here; the driver's 8-GPU run exercises world 8): the
   in-place and out-of-place all-gather of records returns them unchanged.
+- Config C3 whole: the 2^24-pair job as 8 ranks of bench.py (torch.distributed.run, one process per
+  rank, all on this box's GPU, host-staged gather), then in this process the same 2^24 pairs as one
+  contiguous gjkepa_batch and as gjkepa_batch_multi over 8 shards of device 0: every rank's slot of the
+  gathered buffer hashes to the contiguous run's records, and a subsample of every shard matches the
+  oracle.  The reference's own parallelism is its caller's OpenMP loop over GJKEPA (:9, :16).
 """
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
 import numpy as np
 import pytest
 
@@ -17,6 +29,18 @@ import gjkepa
 pytestmark = pytest.mark.gpu
 SEED = 0x6A4B5C1D
 PER_RANK = 1 << 21
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+C3_RANKS = 8
+_c3: dict = {}
+
+
+def _log(msg: str) -> None:
+    """Progress of the long C3 tests, also into gpurun_out/ when it exists (a liveness record)."""
+    print(msg, flush=True)
+    d = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, "c3_progress.log"), "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
 
 
 def _bytes(a):
@@ -122,3 +146,60 @@ def test_two_rank_bench_verifies_its_exchange(tmp_path):
     assert ps["pairs"] == 2 * 2048
     assert sorted(x["rank"] for x in r["per_rank"]) == [0, 1]
     assert all(x["kernel_ms"] > 0 and x["gather_ms"] > 0 for x in r["per_rank"])
+
+
+@pytest.mark.timeout(420)
+def test_c3_whole_job_eight_ranks(tmp_path):
+    """bench.py --gpus 8 (C3: 2^21 pairs per rank, 2^24 in all) under torch.distributed.run: eight
+    processes on this box's one GPU, host-staged all-gather (gloo).  The line checks its own exchange:
+    every rank's hash of every slot agrees, and rank 0's gathered buffer matches the oracle on the first
+    2048 pairs of every shard."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    log = os.path.join(ROOT, "gpurun_out", "c3_bench.log") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) \
+        else str(tmp_path / "c3_bench.log")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(C3_RANKS),
+           "--master-addr", "127.0.0.1", "--master-port", "29553", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(C3_RANKS), "--backend", "gloo", "--steps", "1", "--warmup", "0", "--cpu-sample", "2048"]
+    _log("C3: 8-rank bench starting")
+    with open(log, "w") as lf:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=lf, text=True, timeout=400, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, open(log).read()[-3000:]
+    r = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    _log(f"C3: bench done, {r['value']} M queries/s over {r['n_gpus']} ranks")
+    assert r["n_gpus"] == C3_RANKS and r["config"]["total_pairs"] == C3_RANKS * PER_RANK
+    assert r["config"]["pairs_per_gpu"] == PER_RANK and r["config"]["workload"].startswith("C3")
+    ps = r["parity_sample"]
+    assert ps["gather_consistent"] and ps["all_equal"] and ps["bitexact_records"] == 1.0, ps
+    assert ps["shards"] == C3_RANKS and ps["pairs"] == C3_RANKS * 2048
+    assert sorted(x["rank"] for x in r["per_rank"]) == list(range(C3_RANKS))
+    _c3["slot_sha16"] = {x["rank"]: x["slot_sha16"] for x in r["per_rank"]}
+
+
+@pytest.mark.timeout(420)
+def test_c3_gathered_job_equals_contiguous_run(orc):
+    """The 2^24-pair C3 job in this process: one contiguous gjkepa_batch, and gjkepa_batch_multi over
+    eight shards of device 0 (the one-process multi-device entry), byte-identical to each other; each
+    shard's records hash to the slot the 8-rank bench gathered for that rank; the oracle agrees on 1024
+    pairs spread over every shard."""
+    if "slot_sha16" not in _c3:
+        pytest.skip("needs test_c3_whole_job_eight_ranks")
+    total = C3_RANKS * PER_RANK
+    _log("C3: generating 2^24 pairs")
+    whole = gjkepa.synth_pairs(SEED, total, 32, 32, 2.5)
+    _log("C3: contiguous gjkepa_batch")
+    ref = gjkepa.gjkepa_batch(whole, 2, 1.0)
+    _log("C3: gjkepa_batch_multi over 8 shards of device 0")
+    multi = gjkepa.gjkepa_batch_multi(whole, [0] * C3_RANKS, 2, 1.0)
+    assert multi.tobytes() == ref.tobytes()
+    del multi
+    raw = ref.view(np.uint8).reshape(-1)
+    slot = PER_RANK * ref.itemsize
+    for s in range(C3_RANKS):
+        first, count = gjkepa.shard_range(total, C3_RANKS, s)
+        assert (first, count) == (s * PER_RANK, PER_RANK)
+        h = hashlib.sha256(raw[s * slot:(s + 1) * slot].tobytes()).hexdigest()[:16]
+        assert h == _c3["slot_sha16"][s], s
+        sub = first + np.arange(0, count, count // 1024)[:1024]
+        o = orc.gjkepa_batch(gjkepa.HullPool(whole.verts, whole.hull_off, whole.hull_cnt, whole.pairs[sub]), 2, 1.0)
+        assert ref[sub].tobytes() == o.tobytes(), s
+    _log("C3: contiguous run, 8-shard run and 8-rank gather identical")

@@ -4,8 +4,11 @@
 Runs the C5 workload (hull B offset r ~ U[0, 0.3], 32-128-vertex hulls, every pair a hit) through
 the GPU path in fp64 and fp32 compute, compares both with the fp64 oracle on the same pairs and
 reports: hit / type agreement, the fraction of byte-identical records, and error CDFs of the
-penetration depth (relative) and of the normal (angle), for all pairs and for the subset whose
-final polytope has >= 64 faces.  Also times both precisions on the GPU.  Writes one JSON file.
+penetration depth (relative, and relative to max(1, d)) and of the normal (angle), for all pairs and for
+the subset whose final polytope has >= 64 faces, plus the fp32 gate of tools/fp32_metrics.py on both.
+Runs C5 itself (32-128 vertices) and, as SURVEY §8 d6 suggests to push most pairs past 64 faces, the
+same offsets with 64-128-vertex hulls.  Also times both precisions on the GPU (host API).  Writes one
+JSON file stamped with the library's source hash.
 usage: python tools/c5_sweep.py [n_pairs] [out.json]"""
 import json
 import os
@@ -15,9 +18,11 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "collision-detect-gjk-epa_amd"), os.path.join(ROOT, "oracle")]
+sys.path[:0] = [os.path.join(ROOT, "collision-detect-gjk-epa_amd"), os.path.join(ROOT, "oracle"),
+                os.path.join(ROOT, "tools")]
 import gjkepa  # noqa: E402
 import oracle  # noqa: E402  (checker only)
+from fp32_metrics import fp32_report, passes  # noqa: E402
 
 SEED = 0x6A4B5C1D
 QS = (0.5, 0.9, 0.99, 0.999, 1.0)
@@ -35,6 +40,7 @@ def errors(g, r, mask):
     both = (g["collision"] != 0) & (r["collision"] != 0) & (g["status"] == 0) & (r["status"] == 0)
     gd, rd = g["penetration_depth"][both].astype(np.float64), r["penetration_depth"][both]
     rel = np.abs(gd - rd) / np.maximum(np.abs(rd), 1e-300)
+    unit = np.abs(gd - rd) / np.maximum(np.abs(rd), 1.0)
     gn = g["collision_normal"][both].astype(np.float64)
     rn = r["collision_normal"][both]
     cosang = np.clip(np.sum(gn * rn, axis=1) / np.maximum(np.linalg.norm(gn, axis=1) * np.linalg.norm(rn, axis=1), 1e-300), -1, 1)
@@ -45,15 +51,14 @@ def errors(g, r, mask):
         "type_agreement": float((g["colli_type"] == r["colli_type"]).mean()) if mask.any() else None,
         "status_agreement": float((g["status"] == r["status"]).mean()) if mask.any() else None,
         "depth_rel_err": cdf(rel),
+        "depth_err_over_max1d": cdf(unit),
         "normal_angle_err_rad": cdf(ang),
     }
 
 
-def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
-    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "c5_fp32_sweep.json")
-    pool = gjkepa.synth_pairs(SEED, n, 32, 128, 0.3, dtype=np.float32)
-    res = {"workload": f"C5: {n} pairs, hulls 32-128 vertices, hull B offset r~U[0,0.3], fp32 vertex storage, "
+def sweep(n, nmin, nmax):
+    pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, 0.3, dtype=np.float32)
+    res = {"workload": f"{n} pairs, hulls {nmin}-{nmax} vertices, hull B offset r~U[0,0.3], fp32 vertex storage, "
                        f"version_=2, TOL_FF_=1.0, seed {SEED:#x}", "reference": "fp64 oracle restatement (oracle/)"}
     t = time.perf_counter()
     ref = oracle.gjkepa_batch(pool, 2, 1.0, min(os.cpu_count() or 1, 16))
@@ -61,20 +66,41 @@ def main():
     faces = (ref["diag"] >> 16).astype(np.int64)
     deep = faces >= 64
     res["final_faces"] = {"mean": float(faces.mean()), "frac_ge_64": float(deep.mean()), **cdf(faces)}
+    recs = {}
     for name, prec in (("fp64", gjkepa.PREC_F64), ("fp32", gjkepa.PREC_F32)):
         gjkepa.gjkepa_batch(pool, 2, 1.0, precision=prec)            # warm
         t = time.perf_counter()
         g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=prec)
         dt = time.perf_counter() - t
+        recs[name] = g
         entry = {"host_api_Mq_per_s_incl_transfers": n / dt / 1e6,
                  "all": errors(g, ref, np.ones(n, bool)), "faces_ge_64": errors(g, ref, deep)}
         if prec == gjkepa.PREC_F64:
             entry["bitexact_records"] = float((np.frombuffer(g.tobytes(), np.uint8).reshape(n, -1) ==
                                                np.frombuffer(ref.tobytes(), np.uint8).reshape(n, -1)).all(axis=1).mean())
         res[name] = entry
+    # the fp32 gate (tie-aware normal, depth within 1e-6 max(1, d)) on every pair and on the >= 64-face subset
+    sub = gjkepa.HullPool(pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs[deep])
+    for key, pl, g32, g64 in (("all", pool, recs["fp32"], recs["fp64"]),
+                              ("faces_ge_64", sub, recs["fp32"][deep], recs["fp64"][deep])):
+        rep = fp32_report(pl, g32, g64)
+        rep["gate_passed"] = passes(rep)
+        res["fp32"]["gate_" + key] = rep
+    return res
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "c5_fp32_sweep.json")
+    res = {"lib": gjkepa.version_string(), "src": gjkepa.source_hash(),
+           "C5": sweep(n, 32, 128), "C5_64_128": sweep(n, 64, 128)}
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: (v if k in ("src",) else {"frac_ge_64": v["final_faces"]["frac_ge_64"],
+                                                   "gate_all": v["fp32"]["gate_all"]["gate_passed"],
+                                                   "gate_deep": v["fp32"]["gate_faces_ge_64"]["gate_passed"],
+                                                   "bitexact_fp64": v["fp64"]["bitexact_records"]})
+                      for k, v in res.items() if k != "lib"}))
 
 
 if __name__ == "__main__":
