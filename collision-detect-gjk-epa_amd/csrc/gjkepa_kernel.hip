@@ -30,6 +30,14 @@
 #include "gjkepa_kernel.h"
 #include "gk_common.h"
 
+// Parts of the product build (the host-side launch table below): GK_IN(p) is true when this object
+// compiles part p.
+#ifdef GK_PART
+#define GK_IN(p) (GK_PART == (p))
+#else
+#define GK_IN(p) 1
+#endif
+
 namespace gk {
 
 constexpr int ST_DEFER = 100;   // internal: does not fit this tier
@@ -53,7 +61,7 @@ template <typename T> DEV bool redo_status(int r, bool last_tier) {
 }
 
 // GET_RANDOM_UNIT_VECTOR table (:1578-1689)
-__constant__ double kDirTab[100][3] = {
+[[maybe_unused]] static __constant__ double kDirTab[100][3] = {
 #include "dirtab.inc"
 };
 
@@ -1972,7 +1980,7 @@ template <int G, int SMALL> DEV int tail_unit(int64_t n) {
 // Route tallies (workspace): each wave counts the pairs it routes per code in LDS and adds them to
 // the launch-wide tallies once at its end; a later launch reads its own code's tally to pick dense
 // (single-chunk claims) or sparse (runs of a.claim chunks) scheduling.
-__shared__ uint32_t s_tally[GJKEPA_WS_TALLY];
+static __shared__ uint32_t s_tally[GJKEPA_WS_TALLY];
 DEV void tally_begin() {
     if (lane_id() < GJKEPA_WS_TALLY) s_tally[lane_id()] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -2533,6 +2541,7 @@ __global__ __launch_bounds__(64, 1) void redo_kernel(const gjkepa_epa_args a) {
 // host, which relaunches the grid for the next request), so the grid always drains by itself.
 DEV uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
+#if GK_IN(0)
 __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<64> grp;
@@ -2596,6 +2605,7 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
         if (empty > 4096) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }
     }
 }
+#endif  // GK_IN(0)
 
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
 // finished, from the depth and normal it parked; writes the final record.
@@ -2661,6 +2671,7 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
 }
 
 // Counter / tally reset at the head of a chain (one wave; the chain's first node).
+#if GK_IN(0)
 __global__ __launch_bounds__(64) void ws_reset_kernel(uint32_t* ws, int n32, uint32_t guard) {
 #ifdef GJKEPA_DIAG_GUARD
     const uint32_t g_ = gjkepa_fold(gjkepa_mix(gjkepa_mix(0x72ull, (uint64_t)ws), (uint64_t)(int64_t)n32));
@@ -2669,10 +2680,23 @@ __global__ __launch_bounds__(64) void ws_reset_kernel(uint32_t* ws, int n32, uin
     (void)guard;
     for (int i = (int)threadIdx.x; i < n32; i += 64) ws[i] = 0u;
 }
+#endif  // GK_IN(0)
 
 }  // namespace gk
 
 // ---------------------------------------------------------------- host-side launch table
+// The product build compiles this file once per part (Makefile: -DGK_PART=p), each object instantiating
+// only its own kernels so the parts compile in parallel: 0 = chain reset, query service and the launch
+// dispatchers, 1 = one-wave query path (fp64 compute), 2 = GJK tiers, 3 = contact tiers, 4 + t = EPA
+// tier t, 10 = one-wave query path (fp32 compute), 11 = fp32 redo.
+// Without GK_PART (diagnostic variant builds) one object holds every part.  The non-template kernels
+// (chain reset, query service) are defined in part 0 only.
+// the one-wave query path in fp32 compute (part 10)
+hipError_t gk_launch_query_f32(int vert_dtype, const gjkepa_epa_args& a, hipStream_t s);
+// EPA tier t's launcher, defined in part 4 + t
+#define GK_EPA_DECL(t) hipError_t gk_launch_epa_##t(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s);
+GK_EPA_DECL(0) GK_EPA_DECL(1) GK_EPA_DECL(2) GK_EPA_DECL(3) GK_EPA_DECL(4) GK_EPA_DECL(5)
+static_assert(GJKEPA_EPA_TIERS == 6, "one launcher per EPA tier");
 namespace {
 
 // no more workgroups than the launch has work units: 64-pair chunks, or one wave-round (64 / G
@@ -2689,6 +2713,7 @@ template <typename K_t> int grid_for(K_t kfn, size_t lds, int num_cus, int grid)
     return per_cu * num_cus;
 }
 
+#if GK_IN(2)
 template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     auto kfn = a.warm ? gk::gjk_kernel<TIn, T, G, K, MINW, LH, true> : gk::gjk_kernel<TIn, T, G, K, MINW, LH, false>;
@@ -2699,6 +2724,12 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
+template <typename TIn, typename T>
+hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
+    return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW, (GJKEPA_G0_LH != 0)>(a, s)
+                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW, (GJKEPA_G1_LH != 0)>(a, s);
+}
+#endif
 
 template <typename TIn, typename T, int G, int K, int VC, int FC, int MINW, bool LH, int REFILL = 0, int PR = 0>
 hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
@@ -2717,11 +2748,7 @@ hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
 #define EPA_ARGS(t) GJKEPA_E##t##_G, GJKEPA_E##t##_K, GJKEPA_E##t##_VCAP, GJKEPA_E##t##_FCAP, GJKEPA_E##t##_MINW, \
                     (GJKEPA_E##t##_LH != 0)
 
-template <typename TIn, typename T>
-hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
-    return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW, (GJKEPA_G0_LH != 0)>(a, s)
-                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW, (GJKEPA_G1_LH != 0)>(a, s);
-}
+#if GK_IN(3)
 template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH>;
@@ -2741,27 +2768,45 @@ hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     return tier == 0 ? launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0)>(a, s)
                      : launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0)>(a, s);
 }
+#endif
 
-template <typename TIn, typename T>
-hipError_t epa_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
-    switch (tier) {
-        case 0: return launch_epa<TIn, T, EPA_ARGS(0), GJKEPA_E0_REFILL>(a, s);
-        case 1: return launch_epa<TIn, T, EPA_ARGS(1), GJKEPA_E1_REFILL>(a, s);
-        case 2: return launch_epa<TIn, T, EPA_ARGS(2), GJKEPA_E2_REFILL, GJKEPA_PARK ? 1 : 0>(a, s);   // parks
-        case 3: return launch_epa<TIn, T, EPA_ARGS(3), 0, GJKEPA_PARK ? 1 : 0>(a, s);                  // parks
-        case 4: return launch_epa<TIn, T, EPA_ARGS(4), 0, GJKEPA_PARK ? 2 : 0>(a, s);                  // resumes
-        default: return launch_epa<TIn, T, EPA_ARGS(5)>(a, s);
+// EPA tier t over the four (storage, compute) combinations
+#define GK_EPA_DEF(t, ...)                                                                                        \
+    hipError_t gk_launch_epa_##t(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {          \
+        if (vert_dtype == GJKEPA_DTYPE_F32)                                                                         \
+            return precision == GJKEPA_PREC_F64 ? launch_epa<float, double, __VA_ARGS__>(a, s)                      \
+                                                : launch_epa<float, float, __VA_ARGS__>(a, s);                      \
+        return precision == GJKEPA_PREC_F64 ? launch_epa<double, double, __VA_ARGS__>(a, s)                        \
+                                            : launch_epa<double, float, __VA_ARGS__>(a, s);                         \
     }
-}
 
 }  // namespace
 
+#if GK_IN(4)
+GK_EPA_DEF(0, EPA_ARGS(0), GJKEPA_E0_REFILL)
+#endif
+#if GK_IN(5)
+GK_EPA_DEF(1, EPA_ARGS(1), GJKEPA_E1_REFILL)
+#endif
+#if GK_IN(6)
+GK_EPA_DEF(2, EPA_ARGS(2), GJKEPA_E2_REFILL, GJKEPA_PARK ? 1 : 0)     // parks
+#endif
+#if GK_IN(7)
+GK_EPA_DEF(3, EPA_ARGS(3), 0, GJKEPA_PARK ? 1 : 0)                    // parks
+#endif
+#if GK_IN(8)
+GK_EPA_DEF(4, EPA_ARGS(4), 0, GJKEPA_PARK ? 2 : 0)                    // resumes
+#endif
+#if GK_IN(9)
+GK_EPA_DEF(5, EPA_ARGS(5))
+#endif
+
+#if GK_IN(0)
 hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s) {
     const uint32_t guard = gjkepa_fold(gjkepa_mix(gjkepa_mix(0x72ull, (uint64_t)ws), (uint64_t)(int64_t)n32));
     hipLaunchKernelGGL(gk::ws_reset_kernel, dim3(1), dim3(64), 0, s, ws, n32, guard);
     return hipGetLastError();
 }
-
 #ifdef GJKEPA_DIAG_GUARD
 // diagnostic build only: the argument-guard report ([0] mismatches, [1] kernel id << 8 | route
 // code of the last, [2] expected and [3] recomputed checksum), optionally cleared
@@ -2793,6 +2838,19 @@ hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStrea
     return hipGetLastError();
 }
 
+hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
+    switch (tier) {
+        case 0: return gk_launch_epa_0(vert_dtype, precision, a, s);
+        case 1: return gk_launch_epa_1(vert_dtype, precision, a, s);
+        case 2: return gk_launch_epa_2(vert_dtype, precision, a, s);
+        case 3: return gk_launch_epa_3(vert_dtype, precision, a, s);
+        case 4: return gk_launch_epa_4(vert_dtype, precision, a, s);
+        default: return gk_launch_epa_5(vert_dtype, precision, a, s);
+    }
+}
+#endif
+
+#if GK_IN(1) || GK_IN(10)
 template <typename TIn, typename T> hipError_t launch_query(const gjkepa_epa_args& a, hipStream_t s) {
     // an fp32 query recomputes an uncertified pair in fp64 in place: room for the fp64 image
     using L_t = gk::QLds<TIn, double, GJKEPA_MAX_HULL_VERTS / 64>;
@@ -2800,6 +2858,13 @@ template <typename TIn, typename T> hipError_t launch_query(const gjkepa_epa_arg
     hipLaunchKernelGGL(kfn, dim3((unsigned)a.n_pairs), dim3(64), sizeof(L_t), s, a);
     return hipGetLastError();
 }
+#endif
+#if GK_IN(10)
+hipError_t gk_launch_query_f32(int vert_dtype, const gjkepa_epa_args& a, hipStream_t s) {
+    return vert_dtype == GJKEPA_DTYPE_F32 ? launch_query<float, float>(a, s) : launch_query<double, float>(a, s);
+}
+#endif
+#if GK_IN(11)
 template <typename TIn> hipError_t launch_redo(const gjkepa_epa_args& a, hipStream_t s) {
     using L_t = gk::QLds<TIn, double, GJKEPA_MAX_HULL_VERTS / 64>;
     auto kfn = gk::redo_kernel<TIn>;
@@ -2810,26 +2875,27 @@ template <typename TIn> hipError_t launch_redo(const gjkepa_epa_args& a, hipStre
 hipError_t gjkepa_launch_redo(int vert_dtype, const gjkepa_epa_args& a, hipStream_t s) {
     return vert_dtype == GJKEPA_DTYPE_F32 ? launch_redo<float>(a, s) : launch_redo<double>(a, s);
 }
+#endif
+#if GK_IN(1)
 hipError_t gjkepa_launch_query(int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
-    if (vert_dtype == GJKEPA_DTYPE_F32)
-        return precision == GJKEPA_PREC_F64 ? launch_query<float, double>(a, s) : launch_query<float, float>(a, s);
-    return precision == GJKEPA_PREC_F64 ? launch_query<double, double>(a, s) : launch_query<double, float>(a, s);
+    if (precision != GJKEPA_PREC_F64) return gk_launch_query_f32(vert_dtype, a, s);
+    return vert_dtype == GJKEPA_DTYPE_F32 ? launch_query<float, double>(a, s) : launch_query<double, double>(a, s);
 }
+#endif
 
+#if GK_IN(2)
 hipError_t gjkepa_launch_gjk(int tier, int vert_dtype, int precision, const gjkepa_gjk_args& a, hipStream_t s) {
     if (vert_dtype == GJKEPA_DTYPE_F32)
         return precision == GJKEPA_PREC_F64 ? gjk_any<float, double>(tier, a, s) : gjk_any<float, float>(tier, a, s);
     return precision == GJKEPA_PREC_F64 ? gjk_any<double, double>(tier, a, s) : gjk_any<double, float>(tier, a, s);
 }
 
-hipError_t gjkepa_launch_epa(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
-    if (vert_dtype == GJKEPA_DTYPE_F32)
-        return precision == GJKEPA_PREC_F64 ? epa_any<float, double>(tier, a, s) : epa_any<float, float>(tier, a, s);
-    return precision == GJKEPA_PREC_F64 ? epa_any<double, double>(tier, a, s) : epa_any<double, float>(tier, a, s);
-}
+#endif
 
+#if GK_IN(3)
 hipError_t gjkepa_launch_contact(int tier, int vert_dtype, int precision, const gjkepa_epa_args& a, hipStream_t s) {
     if (vert_dtype == GJKEPA_DTYPE_F32)
         return precision == GJKEPA_PREC_F64 ? contact_any<float, double>(tier, a, s) : contact_any<float, float>(tier, a, s);
     return precision == GJKEPA_PREC_F64 ? contact_any<double, double>(tier, a, s) : contact_any<double, float>(tier, a, s);
 }
+#endif

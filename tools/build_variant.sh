@@ -8,8 +8,13 @@ D=collision-detect-gjk-epa_amd
 OUT=${VARDIR:-$D/build/variants}/$NAME
 mkdir -p $OUT
 F="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $*"
-/opt/rocm/bin/hipcc $F -c $D/csrc/gjkepa_kernel.hip -o $OUT/k.o
+# the narrow-phase kernels in their parts (GK_PART, as the Makefile builds them), in parallel
+PIDS=""
+for p in 0 1 2 3 4 5 6 7 8 9 10 11; do
+  /opt/rocm/bin/hipcc $F -DGK_PART=$p -c $D/csrc/gjkepa_kernel.hip -o $OUT/k$p.o & PIDS="$PIDS $!"
+done
 /opt/rocm/bin/hipcc $F -DGJKEPA_SRC_HASH="\"variant-$NAME\"" -c $D/csrc/gjkepa_capi.cpp -o $OUT/c.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k.o $OUT/c.o $D/build/hull_kernel.o \
+for pid in $PIDS; do wait $pid; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fopenmp $OUT/k[0-9]*.o $OUT/c.o $D/build/hull_kernel.o \
     $D/build/broadphase_kernel.o $D/build/contacts_kernel.o $D/build/gjkepa_multi.o $D/build/synth.o -o $OUT/libgjkepa_hip.so -ldl -pthread -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo built $OUT/libgjkepa_hip.so
