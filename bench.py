@@ -76,7 +76,7 @@ def moved_copy(pool, delta: float, seed: int) -> np.ndarray:
     return v.astype(pool.verts.dtype)
 
 
-WS_COUNTERS, WS_TALLY = 32, 48          # gjkepa_kernel.h: workspace header (uint32 words)
+WS_COUNTERS, WS_TALLY = 40, 48          # gjkepa_kernel.h: workspace header (uint32 words)
 ROUTE_EPA0, ROUTE_CT0 = 0x10, 0x20
 
 
@@ -97,24 +97,35 @@ def served_pairs(r, tally: np.ndarray, recs, shares: dict) -> float:
     return tot
 
 
+def busy_span(rs) -> float:
+    """Time covered by the union of the launches' [start, end] intervals (concurrent launches once)."""
+    iv = sorted((float(r["start_ms"]), float(r["end_ms"])) for r in rs)
+    tot, cs, ce = 0.0, None, None
+    for s, e in iv:
+        if ce is None or s > ce:
+            if ce is not None:
+                tot += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    return tot + (ce - cs if ce is not None else 0.0)
+
+
 def dominant_kernel(lt: np.ndarray, tally: np.ndarray, recs, bpq: float, pmc: dict | None) -> dict:
-    """The kernel (kind, tier) whose launches span the most time per chain, from the launch timing of the
-    timed steps (gjkepa_launch_timing_read records)."""
+    """The kernel (kind, tier) with the most launch time per chain (sum of its launches' durations), from
+    the launch timing of the measured steps (gjkepa_launch_timing_read records); its wall span is the
+    union of its launches' intervals per chain (two concurrent parts count once)."""
     chains = sorted(set(int(c) for c in lt["chain"]))
     groups: dict = {}
     for r in lt:
         groups.setdefault((r["kernel"].decode(), int(r["tier"])), []).append(r)
-    best, best_span = None, -1.0
+    best, best_busy = None, -1.0
     for key, rs in groups.items():
-        spans = []
-        for c in chains:
-            cr = [r for r in rs if int(r["chain"]) == c]
-            if cr:
-                spans.append(max(float(r["end_ms"]) for r in cr) - min(float(r["start_ms"]) for r in cr))
-        span = float(np.mean(spans)) if spans else 0.0
-        if span > best_span:
-            best, best_span = key, span
+        busy = sum(float(r["end_ms"]) - float(r["start_ms"]) for r in rs) / len(chains)
+        if busy > best_busy:
+            best, best_busy = key, busy
     rs = groups[best]
+    best_span = float(np.mean([busy_span([r for r in rs if int(r["chain"]) == c]) for c in chains]))
     # parts of one route code in several pair ranges: hits per range apportion the code's tally
     by_code: dict = {}
     for r in rs:
@@ -142,7 +153,7 @@ def dominant_kernel(lt: np.ndarray, tally: np.ndarray, recs, bpq: float, pmc: di
            "method": "HIP events around each launch (gjkepa_launch_timing) over the timed steps; pairs = the "
                      "launch's route-code tally in the workspace (parts: split by the hits in each part's range); "
                      "achieved = pairs per launch x bytes per pair / mean launch duration; span_* = per step, "
-                     "over the wall span from the first launch's start to the last one's end"}
+                     "over the wall time its launches cover (the union of their intervals)"}
     # the same kernel in the committed PMC run (same library source hash): its traffic per launch and its
     # VALU-busy share priced against the wall span of its launches
     if pmc:
@@ -288,8 +299,10 @@ def parse():
     ap.add_argument("--legs", default="C4,C5", help="N=1: extra configs run on the same GPU after the main one "
                                                    "(comma list; 'none' to skip)")
     ap.add_argument("--leg-sample", type=int, default=65536, help="pairs of each leg checked against the oracle")
-    ap.add_argument("--launch-timing", choices=["timed", "separate", "off"], default="timed",
-                    help="timed: launch events inside the timed steps; separate: in a second pass of the same steps")
+    ap.add_argument("--launch-timing", choices=["timed", "separate", "off"], default="separate",
+                    help="separate (default): the launch events in a second pass of the same steps right after the "
+                         "timed ones (they cost ~0.9%% on C2 when inside: profiles/r05/ab_launch_timing.txt); "
+                         "timed: inside the timed steps")
     return ap.parse_args()
 
 
@@ -316,12 +329,18 @@ def run_leg(cfg: str, args, dev, stream, prec: int, lib_src: str) -> dict:
         launch()
     torch.cuda.synchronize(dev)
     steps = max(1, min(args.steps, 10))
-    gjkepa.launch_timing(True)
+    inside = args.launch_timing == "timed"
+    gjkepa.launch_timing(inside)
     t0 = time.perf_counter()
     for _ in range(steps):
         launch()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    if not inside:                                  # the same steps once more, with the launch events
+        gjkepa.launch_timing(True)
+        for _ in range(steps):
+            launch()
+        torch.cuda.synchronize(dev)
     gjkepa.launch_timing(False)
     lt = gjkepa.launch_timing_read()
     recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=gjkepa.record_dtype(prec))

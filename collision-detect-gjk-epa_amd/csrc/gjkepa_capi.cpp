@@ -301,12 +301,15 @@ int epa2_parts() {
     static const int p = parts_env("GJKEPA_EPA2_PARTS", GJKEPA_EPA2_PARTS);
     return p;
 }
+// launches of a contact pass with `tiers` contact tiers: a one-tier pass adds the case_04 pass its main
+// launch defers to (GJKEPA_C0_DEFER04; with two tiers, contact tier 1 takes those pairs)
+constexpr int contact_launches(int tiers) { return tiers == 1 && GJKEPA_C0_DEFER04 ? 2 : tiers; }
 // launches of an overlapped chain: 2 GJK + the EPA tiers (tiers 0 and 2 in up to kPartsMax parts) +
 // each fork point's contact pass (once per part); every launch owns one workspace counter
 constexpr int overlap_launches() {
     int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS + 2 * (kPartsMax - 1);
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
-        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t) * (t == 0 || t == 2 ? kPartsMax : 1);
+        if ((GJKEPA_FORK_MASK >> t) & 1) n += contact_launches(fork_contact_tiers(t)) * (t == 0 || t == 2 ? kPartsMax : 1);
     return n;
 }
 static_assert(overlap_launches() + 1 <= GJKEPA_WS_COUNTERS, "workspace launch counters (+1: the fp32 redo launch)");
@@ -325,7 +328,7 @@ static_assert(GJKEPA_ROUTE_REDO < GJKEPA_WS_TALLY && GJKEPA_ROUTE_REDO > GJKEPA_
 // tier 3 would outgrow its 40-vertex polytope anyway; which tier answers never changes a record).
 // Environment override GJKEPA_E23_STREAMS for A/B.
 #ifndef GJKEPA_E23_STREAMS
-#define GJKEPA_E23_STREAMS 2
+#define GJKEPA_E23_STREAMS 1       // A/B r5 (C4, 2 rounds): in sequence 39.51 / 39.41, side by side 38.54 / 38.63 M/s; C5 within 0.2%
 #endif
 int e23_streams() {
     static const int p = [] {
@@ -475,13 +478,15 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     if ((e = timed("gjk", 0, 0, -1, 0, n_pairs, s, [&] { return gjkepa_launch_gjk(0, vert_dtype, precision, g, s); })) !=
         hipSuccess)
         return hip_fail(e, "GJK tier 0 launch");
-    g.route_code = GJKEPA_ROUTE_GJK1;                    // GJK tier 1: hulls above tier 0's capacity
-    g.ctr = ctr + launch++;
-    g.claim = kSparseClaim;
-    g.guard = gjkepa_guard_of(g);
-    if ((e = timed("gjk", 1, 0, g.route_code, 0, n_pairs, s, [&] { return gjkepa_launch_gjk(1, vert_dtype, precision, g, s); })) !=
-        hipSuccess)
-        return hip_fail(e, "GJK tier 1 launch");
+    for (int t = 1; t < GJKEPA_GJK_TIERS; ++t) {         // GJK tiers 1, 2: hulls above tier 0's capacity
+        g.route_code = GJKEPA_ROUTE_GJK1 + t - 1;
+        g.ctr = ctr + launch++;
+        g.claim = kSparseClaim;
+        g.guard = gjkepa_guard_of(g);
+        if ((e = timed("gjk", t, 0, g.route_code, 0, n_pairs, s, [&] { return gjkepa_launch_gjk(t, vert_dtype, precision, g, s); })) !=
+            hipSuccess)
+            return hip_fail(e, "GJK tier launch");
+    }
     gjkepa_epa_args a{};
     a.version = version;
     a.tol_ff = tol_ff;
@@ -544,6 +549,17 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
             hipError_t er = timed("contact", t, part, a.route_code, r_first, a.n_pairs, cs,
                                   [&] { return gjkepa_launch_contact(t, vert_dtype, precision, a, cs); });
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
+        }
+        if (ntiers == 1 && GJKEPA_C0_DEFER04) {           // the case_04 pairs contact tier 0 left: base + 1
+            a.route_code = base + 1;
+            a.next_code = -1;
+            a.ctr = ctr + launch++;
+            a.claim = single ? 1 : kSparseClaim;
+            a.grid = 0;
+            a.guard = gjkepa_guard_of(a);
+            hipError_t er = timed("contact", GJKEPA_CONTACT_C04, part, a.route_code, r_first, a.n_pairs, cs,
+                                  [&] { return gjkepa_launch_contact(GJKEPA_CONTACT_C04, vert_dtype, precision, a, cs); });
+            if (er != hipSuccess) return hip_fail(er, "contact case_04 pass launch");
         }
         return 0;
     };
@@ -736,17 +752,17 @@ const char* gjkepa_last_error(void) { return g_err.c_str(); }
 const char* gjkepa_version_string(void) {
     static char buf[800];
     std::snprintf(buf, sizeof(buf),
-                  "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
+                  "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
                   "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
-                  "waves/SIMD G%d%d E%d%d%d%d%d%d C%d%d; LDS-hull G%d%d E%d%d%d%d%d%d C%d%d; "
+                  "waves/SIMD G%d%d%d E%d%d%d%d%d%d C%d%d%d; LDS-hull G%d%d%d E%d%d%d%d%d%d C%d%d; "
                   "-O3 -ffp-contract=off; src %s",
-                  GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
+                  GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G2_G, GJKEPA_G2_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
                   GJKEPA_E2_VCAP, GJKEPA_E2_FCAP, GJKEPA_E3_G, GJKEPA_E3_K, GJKEPA_E3_VCAP, GJKEPA_E3_FCAP,
                   GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_E5_G, GJKEPA_E5_K, GJKEPA_E5_VCAP,
                   GJKEPA_E5_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
-                  GJKEPA_C1_K, GJKEPA_G0_MINW, GJKEPA_G1_MINW, GJKEPA_E0_MINW, GJKEPA_E1_MINW, GJKEPA_E2_MINW,
-                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_E5_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH,
+                  GJKEPA_C1_K, GJKEPA_G0_MINW, GJKEPA_G1_MINW, GJKEPA_G2_MINW, GJKEPA_E0_MINW, GJKEPA_E1_MINW, GJKEPA_E2_MINW,
+                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_E5_MINW, GJKEPA_C0M_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH, GJKEPA_G2_LH,
                   GJKEPA_E0_LH, GJKEPA_E1_LH, GJKEPA_E2_LH, GJKEPA_E3_LH, GJKEPA_E4_LH, GJKEPA_E5_LH, GJKEPA_C0_LH,
                   GJKEPA_C1_LH, GJKEPA_SRC_HASH);
     return buf;

@@ -25,14 +25,25 @@
 #ifndef GJKEPA_G0_MINW
 #define GJKEPA_G0_MINW 2        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
 #endif
+// GJK tier 1: hulls of 33-128 vertices (C5, a quarter of C4); GJK tier 2: up to 256.  A pair goes to
+// the smallest tier that holds its larger hull, so a 128-vertex pair scans 4 vertices per lane, not 8.
 #ifndef GJKEPA_G1_G
-#define GJKEPA_G1_G 32          // two pairs per wave (A/B on C4: 26.3 vs 25.5M queries/s at 64 lanes x 4)
+#define GJKEPA_G1_G 32
 #endif
 #ifndef GJKEPA_G1_K
-#define GJKEPA_G1_K 8
+#define GJKEPA_G1_K 4
 #endif
 #ifndef GJKEPA_G1_MINW
-#define GJKEPA_G1_MINW 3           // LDS hull frees the 96 VGPRs of register copies: three waves per SIMD
+#define GJKEPA_G1_MINW 3
+#endif
+#ifndef GJKEPA_G2_G
+#define GJKEPA_G2_G 32          // two pairs per wave (A/B on C4: 26.3 vs 25.5M queries/s at 64 lanes x 4)
+#endif
+#ifndef GJKEPA_G2_K
+#define GJKEPA_G2_K 8
+#endif
+#ifndef GJKEPA_G2_MINW
+#define GJKEPA_G2_MINW 3           // LDS hull frees the 96 VGPRs of register copies: three waves per SIMD
 #endif
 // EPA tiers: G, K as above, EPA polytope capacity VCAP vertices / FCAP faces
 #ifndef GJKEPA_E0_G
@@ -153,6 +164,16 @@
 #ifndef GJKEPA_C0_MINW
 #define GJKEPA_C0_MINW 2
 #endif
+// contact tier 0's main pass leaves contact v2's case_04 (SORT_CLOCK and the polygon containment test,
+// about a quarter of C2's hits) to a full pass of the same hull shape (GJKEPA_CONTACT_C04) or to contact
+// tier 1, so it fits GJKEPA_C0M_MINW waves per SIMD; 0: one full tier-0 pass (A/B)
+#ifndef GJKEPA_C0_DEFER04
+#define GJKEPA_C0_DEFER04 1
+#endif
+#ifndef GJKEPA_C0M_MINW
+#define GJKEPA_C0M_MINW (GJKEPA_C0_DEFER04 ? 3 : GJKEPA_C0_MINW)
+#endif
+#define GJKEPA_CONTACT_C04 2    // gjkepa_launch_contact: the tier-0-shaped full pass over route code CT(p) + 1
 #ifndef GJKEPA_C1_G
 #define GJKEPA_C1_G 64
 #endif
@@ -198,7 +219,10 @@
 #define GJKEPA_G0_LH 1
 #endif
 #ifndef GJKEPA_G1_LH
-#define GJKEPA_G1_LH 1             // A/B r4 (2 rounds, with G1_MINW 3): C4 39.07 -> 39.54, C2 -0.2%, C5 -0.4%
+#define GJKEPA_G1_LH 1
+#endif
+#ifndef GJKEPA_G2_LH
+#define GJKEPA_G2_LH 1             // A/B r4 (2 rounds, with MINW 3): C4 39.07 -> 39.54, C2 -0.2%, C5 -0.4%
 #endif
 #ifndef GJKEPA_E0_LH
 #define GJKEPA_E0_LH 1
@@ -227,20 +251,20 @@
 #ifndef GJKEPA_CONTACT_OVERLAP
 #define GJKEPA_CONTACT_OVERLAP 1    // each EPA tier's contact pass on a second stream, overlapping the later EPA tiers
 #endif
-#define GJKEPA_GJK_TIERS 2
+#define GJKEPA_GJK_TIERS 3
 #define GJKEPA_EPA_TIERS 6
 #define GJKEPA_CONTACT_TIERS 2
 
 // workspace: a 512-byte header of per-launch chunk counters, route tallies and the park counter, then
 // one route byte per pair, then park slots (gjkepa_capi.cpp, gjkepa_workspace_bytes)
-#define GJKEPA_WS_COUNTERS 32   // uint32 counters at the head of the workspace (one per launch of a chain)
+#define GJKEPA_WS_COUNTERS 40   // uint32 counters at the head of the workspace (one per launch of a chain)
 // then GJKEPA_WS_TALLY uint32 route tallies (indexed by route code): every kernel adds the pairs it
 // routes on; a launch whose own tally is at least 1/16 of the batch claims single chunks (dense),
 // otherwise runs of `claim` chunks (sparse scan)
 #define GJKEPA_WS_TALLY 48
 // route byte per pair (workspace): which kernel owns the pair next
 #define GJKEPA_ROUTE_DONE 0
-#define GJKEPA_ROUTE_GJK1 1
+#define GJKEPA_ROUTE_GJK1 1         // + GJK tier - 1 (tiers 1, 2)
 #define GJKEPA_ROUTE_EPA0 0x10      // + EPA tier
 #define GJKEPA_ROUTE_CT0 0x20       // + contact tier
 // with GJKEPA_CONTACT_OVERLAP, the pairs EPA tier t finishes go to contact tier c under code CT(t) + c

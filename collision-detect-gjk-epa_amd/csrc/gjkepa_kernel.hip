@@ -43,6 +43,7 @@ namespace gk {
 constexpr int ST_DEFER = 100;   // internal: does not fit this tier
 constexpr int ST_REDO = 103;    // internal (fp32 compute): answer not certified, recompute in fp64
 constexpr int ST_PARKED = 104;  // internal: polytope parked for the next tier (gjkepa_kernel.h "Polytope parking")
+constexpr int ST_CASE04 = 105;  // internal: contact v2 case_04, left to the full contact pass (contact_kernel DEFER04)
 
 // fp32 certificate.  An fp32 EPA can build an invalid polytope from inconsistent visibility decisions
 // on near-coplanar faces (the fp32 rounding of a sliver's normal), after which its MINLOC distance
@@ -1444,8 +1445,11 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
     return 0;
 }
 
-// get_collisionPoint_02 (:457-696)
-CTX_T DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
+// get_collisionPoint_02 (:457-696).  DEFER04: case_04 (SORT_CLOCK + polygon containment, a quarter of
+// C2's hits) is not computed here: ST_CASE04 hands the pair to the full contact pass, so the common
+// kernel does not carry case_04's registers (contact_kernel).
+template <bool DEFER04 = false, typename T, typename TH, int G, int K, int VC, int FC, int LH>
+DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
     auto& C = c.L.u.c;
     const T band = T(0.1);
     const T t1 = D.m[0] - band, t2 = D.m[1] - band;                 // :471-472
@@ -1472,6 +1476,8 @@ CTX_T DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
         V3<T> f1, f2;
         foot_ll(a0, a1, vmk<T>(C.sx[0], C.sy[0], C.sz[0]), vmk<T>(C.sx[1], C.sy[1], C.sz[1]), f1, f2);
         res = vdiv(vadd(f1, f2), T(2));
+    } else if (DEFER04 && ((n1 == 2 && n2 >= 3) || (n1 >= 3 && n2 == 2))) {
+        return ST_CASE04;
     } else if (n1 == 2 && n2 >= 3) {                               // case_04(SPT_p2, SPT_p1)
         band_set(c, 0, D, t1, true);
         const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
@@ -1784,7 +1790,8 @@ CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t
 
 // EPA_solu's post-processing (:326-343) for EPA depth and normal n: nearest points, contact point
 // (version_ 1/2/3) and contact type.  Returns -type (o13 filled) or an error status.
-CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
+template <bool DEFER04 = false, typename T, typename TH, int G, int K, int VC, int FC, int LH>
+DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
     int st;
     int ia, ib;
     GK_STAMP(SE_TERM);
@@ -1796,7 +1803,7 @@ CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* 
     V3<T> pt = zero3<T>();
     bool same_n = true;
     if (version == 1) st = contact_v1(c, n, D, pt);                       // :329-340
-    else if (version == 2) st = contact_v2(c, D, pt);
+    else if (version == 2) st = contact_v2<DEFER04>(c, D, pt);
     else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; same_n = false; }
     else st = GJKEPA_STATUS_BAD_VERSION;
     GK_STAMP(SE_CONT);
@@ -2103,8 +2110,8 @@ __global__ __launch_bounds__(64, MINW) void gjk_kernel(const gjkepa_gjk_args a) 
         if (na < 1 || nb < 1 || na > GJKEPA_MAX_HULL_VERTS || nb > GJKEPA_MAX_HULL_VERTS) {
             store_record<G, T>(a.out, pair, gl, o13, 0, 0, GJKEPA_STATUS_BAD_INPUT, 0u);
             if (WARM && gl < 4) a.warm[4 * pair + gl] = kStale;
-        } else if (na > K * G || nb > K * G) {
-            next = GJKEPA_ROUTE_GJK1;                        // larger GJK tier
+        } else if (na > K * G || nb > K * G) {             // the smallest larger GJK tier that holds both
+            next = (uint8_t)((na > nb ? na : nb) <= GJKEPA_G1_G * GJKEPA_G1_K ? GJKEPA_ROUTE_GJK1 : GJKEPA_ROUTE_GJK1 + 1);
         } else {
             c.na = na;
             c.nb = nb;
@@ -2608,8 +2615,11 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
 #endif  // GK_IN(0)
 
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
-// finished, from the depth and normal it parked; writes the final record.
-template <typename TIn, typename T, int G, int K, int MINW, bool LH>
+// finished, from the depth and normal it parked; writes the final record.  DEFER04 (contact tier 0's
+// main pass): a version-2 pair that takes case_04 goes on to route code route_code + 1 unanswered — the
+// full pass of the same fork point (contact tier 1, or the tier-0-shaped case_04 pass) — so this kernel
+// fits three waves per SIMD (158 VGPRs instead of 256).
+template <typename TIn, typename T, int G, int K, int MINW, bool LH, bool DEFER04>
 __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, 0, 1>;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -2639,11 +2649,13 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
 #else
-        const int r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
+        const int r = contact_phase<DEFER04>(c, depth, n, a.version, (T)a.tol_ff, o13);
 #endif
         __builtin_amdgcn_wave_barrier();
         uint8_t next = 0;
-        if (r < 0) {
+        if (DEFER04 && r == ST_CASE04) {
+            next = (uint8_t)(a.route_code + 1);
+        } else if (r < 0) {
             store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
         } else if (redo_status<T>(r, false)) {   // fp32: contact-phase error, recomputed in fp64
             next = GJKEPA_ROUTE_REDO;
@@ -2726,8 +2738,10 @@ hipError_t launch_gjk(const gjkepa_gjk_args& a, hipStream_t s) {
 }
 template <typename TIn, typename T>
 hipError_t gjk_any(int tier, const gjkepa_gjk_args& a, hipStream_t s) {
+    static_assert(GJKEPA_GJK_TIERS == 3 && GJKEPA_G2_G * GJKEPA_G2_K >= GJKEPA_MAX_HULL_VERTS, "the last GJK tier holds every hull");
     return tier == 0 ? launch_gjk<TIn, T, GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G0_MINW, (GJKEPA_G0_LH != 0)>(a, s)
-                     : launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW, (GJKEPA_G1_LH != 0)>(a, s);
+         : tier == 1 ? launch_gjk<TIn, T, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G1_MINW, (GJKEPA_G1_LH != 0)>(a, s)
+                     : launch_gjk<TIn, T, GJKEPA_G2_G, GJKEPA_G2_K, GJKEPA_G2_MINW, (GJKEPA_G2_LH != 0)>(a, s);
 }
 #endif
 
@@ -2749,9 +2763,9 @@ hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
                     (GJKEPA_E##t##_LH != 0)
 
 #if GK_IN(3)
-template <typename TIn, typename T, int G, int K, int MINW, bool LH>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH, bool DEFER04>
 hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
-    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH>;
+    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH, DEFER04>;
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 1>, G>() * GPW;
     int grid;
@@ -2763,10 +2777,15 @@ hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
+// tier 0: the main small-hull pass (case_04 deferred to route code + 1); 1: large hulls (full);
+// GJKEPA_CONTACT_C04: the small-hull full pass for the deferred case_04 pairs
 template <typename TIn, typename T>
 hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
-    return tier == 0 ? launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0)>(a, s)
-                     : launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0)>(a, s);
+    if (tier == 0)
+        return launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0M_MINW, (GJKEPA_C0_LH != 0), (GJKEPA_C0_DEFER04 != 0)>(a, s);
+    if (tier == GJKEPA_CONTACT_C04)
+        return launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0), false>(a, s);
+    return launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0), false>(a, s);
 }
 #endif
 

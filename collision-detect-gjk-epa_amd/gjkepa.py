@@ -41,7 +41,7 @@ EXPORTS = (
 COMM_ID_BYTES = 128
 # workspace header word counting the park slots a gjkepa_batch_device call took (diagnostics; csrc/
 # gjkepa_capi.cpp kWsParkWord = GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY)
-WS_PARK_WORD = 32 + 48
+WS_PARK_WORD = 40 + 48
 HULL_MAX_POINTS = 256
 
 REC64 = np.dtype([

@@ -155,3 +155,48 @@ def test_batches_finish_beside_sustained_queries(orc):
             x.join()
     assert max(times) < 1.0, times
     assert sum(counts) > 100
+
+
+def _checked_traffic(stop_evt, qs, out):
+    """One caller thread: single-pair calls in a loop until stop_evt is set, keeping (index, contact)."""
+    i = 0
+    while not stop_evt.is_set():
+        out.append((i % len(qs), gjkepa.gjkepa(*qs[i % len(qs)])))
+        i += 1
+
+
+@pytest.mark.gpu
+def test_service_off_while_calls_in_flight(orc):
+    """gjkepa_query_service_set(0) while four threads keep calling: a call in flight is
+    answered by the draining grid or finishes through the combining path — none relaunches the grid — so
+    a device-wide synchronisation right after the callers stop does not wait for a resident grid; every
+    answer is the oracle's.  Turning the service back on brings the grid back."""
+    import torch
+    qs = _big_pairs(24, 47, 4, 40)
+    stop_evt = threading.Event()
+    outs = [[] for _ in range(4)]
+    th = [threading.Thread(target=_checked_traffic, args=(stop_evt, qs, o)) for o in outs]
+    for x in th:
+        x.start()
+    try:
+        time.sleep(0.1)
+        assert gjkepa.query_service_set(False) is True
+        time.sleep(0.1)                        # calls keep coming: combined now
+    finally:
+        stop_evt.set()
+        for x in th:
+            x.join()
+    t = time.perf_counter()
+    torch.cuda.synchronize()
+    t_sync = time.perf_counter() - t
+    try:
+        assert t_sync < 0.0015, f"synchronize with the service off took {t_sync * 1e3:.2f} ms"
+        got = [c for o in outs for _, c in o]
+        idx = [k for o in outs for k, _ in o]
+        assert len(got) > 50
+        ref = {k: orc.gjkepa(*qs[k]) for k in set(idx)}
+        bad = [j for j, (k, c) in enumerate(zip(idx, got)) if not _same(c, ref[k])]
+        assert not bad, f"{len(bad)} mismatches"
+    finally:
+        assert gjkepa.query_service_set(True) is False
+    _check(orc, qs[:4], [gjkepa.gjkepa(*q) for q in qs[:4]])
