@@ -1154,13 +1154,14 @@ int service_ensure(Service* sv, bool check_done, int slot) {
 
 // GJKEPA_QUERY_STATS=1: calls served, mean round trip and mean device time per call, printed at exit
 struct ServiceStats {
-    std::atomic<int64_t> calls{0}, ns{0}, dev_ticks{0}, tick_khz{0};
+    std::atomic<int64_t> calls{0}, ns{0}, dev_ticks{0}, tick_khz{0}, declined{0};
     bool on = std::getenv("GJKEPA_QUERY_STATS") != nullptr;
     ~ServiceStats() {
         if (on && calls > 0 && tick_khz > 0)
-            std::fprintf(stderr, "gjkepa_query service: %lld calls, %.2f us/call round trip, %.2f us/call on the device\n",
+            std::fprintf(stderr, "gjkepa_query service: %lld calls, %.2f us/call round trip, %.2f us/call on the device, "
+                                 "%lld declined\n",
                          (long long)calls.load(), 1e-3 * (double)ns / (double)calls,
-                         1e3 * (double)dev_ticks / (double)tick_khz / (double)calls);
+                         1e3 * (double)dev_ticks / (double)tick_khz / (double)calls, (long long)declined.load());
     }
 } g_sstats;
 
@@ -1251,7 +1252,7 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
     int rc = 0;
     Query me{version, tol_ff, p1, p2, n1, n2, {}};
-    Service* sv = service_enabled() && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS &&
+    Service* sv = service_enabled() && n1 >= 1 && n2 >= 1 && n1 <= GJKEPA_SVC_MAX_HULL && n2 <= GJKEPA_SVC_MAX_HULL &&
                   device >= 0 && device < device_count_cached() ? service(device) : nullptr;
     const int slot = sv ? service_claim(sv) : -1;
     bool served = false;
@@ -1265,7 +1266,10 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
         else
             sv->stuck.fetch_or(1ull << slot, std::memory_order_release);
         if (rc != 0 && rc != kSvcOff) return rc;
-        served = rc == 0;
+        // a pair the service's lean path declined (its polytope outgrew the small one) is recomputed on
+        // the combining path, which runs the full one-wave path
+        served = rc == 0 && me.rec.status != GJKEPA_SVC_DECLINED;
+        if (g_sstats.on && rc == 0 && !served) g_sstats.declined += 1;
     }
     if (!served && !device_state(device, &rc)) return rc;
     if (!served) {

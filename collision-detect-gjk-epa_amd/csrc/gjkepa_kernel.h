@@ -168,7 +168,7 @@
 // about a quarter of C2's hits) to a full pass of the same hull shape (GJKEPA_CONTACT_C04) or to contact
 // tier 1, so it fits GJKEPA_C0M_MINW waves per SIMD; 0: one full tier-0 pass (A/B)
 #ifndef GJKEPA_C0_DEFER04
-#define GJKEPA_C0_DEFER04 1
+#define GJKEPA_C0_DEFER04 0     // A/B r5 (C2, 2 rounds): one full pass 158.5 / 158.7, deferred 151.9 / 151.9 M/s (3 waves/SIMD, 158 VGPRs)
 #endif
 #ifndef GJKEPA_C0M_MINW
 #define GJKEPA_C0M_MINW (GJKEPA_C0_DEFER04 ? 3 : GJKEPA_C0_MINW)
@@ -384,6 +384,21 @@ hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s);
 // completion line by the device (record first, `done` last, release); each side polls the other's.
 #ifndef GJKEPA_SVC_SLOTS
 #define GJKEPA_SVC_SLOTS 64
+#endif
+// The service's waves run a lean one-wave path: hulls of up to GJKEPA_SVC_MAX_HULL vertices (two hull
+// vertices per lane) and EPA's small first polytope only, so a resident wave reserves ~half the
+// registers and a third of the LDS of the full path (what it costs a concurrent batch).  A pair whose
+// polytope outgrows the small one is declined (record status GJKEPA_SVC_DECLINED) and recomputed by
+// the caller on the combining path; larger hulls go there directly.  Records never differ.
+#ifndef GJKEPA_SVC_LEAN
+#define GJKEPA_SVC_LEAN 1        // 0: the full one-wave path (every hull size, restart with the large polytope; A/B)
+#endif
+#ifndef GJKEPA_SVC_MAX_HULL
+#define GJKEPA_SVC_MAX_HULL (GJKEPA_SVC_LEAN ? 128 : GJKEPA_MAX_HULL_VERTS)
+#endif
+#define GJKEPA_SVC_DECLINED 0x7E
+#ifndef GJKEPA_SVC_MINW
+#define GJKEPA_SVC_MINW (GJKEPA_SVC_LEAN ? 3 : 1)   // lean: 168 VGPRs (21 spilled) instead of 196 (full path: 249)
 #endif
 struct alignas(128) gjkepa_svc_slot {
     uint32_t req, stop;              // posted request's sequence number; nonzero: the serving wave exits

@@ -25,6 +25,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/gjkepa.h"
 #include "gjkepa_kernel.h"
@@ -2414,7 +2415,9 @@ template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEP
 template <typename TIn, typename T, int K> using QLdsS = Lds<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, true>;
 // RT: the record's field type (T, or float for the fp32 chain's fp64 redo).  Returns true when an fp32
 // answer is not certified (certify<T>(): nothing stored; the caller recomputes the pair in fp64).
-template <typename TIn, typename T, int K, typename RT = T>
+// LEAN (the resident service): no restart with the last tier's polytope; an overflowing pair is stored
+// with status GJKEPA_SVC_DECLINED for the caller to recompute on the full path.
+template <typename TIn, typename T, int K, typename RT = T, bool LEAN = false>
 DEV bool query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
                       int version, T tol_ff, void* out, int64_t pair) {
     using LB = QLds<TIn, T, K>;
@@ -2451,7 +2454,12 @@ DEV bool query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, co
     uint32_t de = 0;
     r = epa_phase(c, kc, depth, n, de);
     __builtin_amdgcn_wave_barrier();
-    if (r == ST_DEFER) {                                 // small polytope full: the last tier's from the simplex
+    if constexpr (LEAN) {
+        if (r == ST_DEFER) {                             // declined: the caller runs the full path
+            store_record<64, RT>(out, pair, gl, o, 0, 0, GJKEPA_SVC_DECLINED, 0u);
+            return false;
+        }
+    } else if (r == ST_DEFER) {                          // small polytope full: the last tier's from the simplex
         Ctx<T, TIn, 64, K, GJKEPA_E5_VCAP, GJKEPA_E5_FCAP, 2> cb{*reinterpret_cast<QLds<TIn, T, K>*>(smem), grp};
         cb.na = na;
         cb.nb = nb;
@@ -2549,7 +2557,7 @@ __global__ __launch_bounds__(64, 1) void redo_kernel(const gjkepa_epa_args a) {
 DEV uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
 #if GK_IN(0)
-__global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a) {
+__global__ __launch_bounds__(64, GJKEPA_SVC_MINW) void service_kernel(const gjkepa_svc_args a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const Grp<64> grp;
     gjkepa_svc_slot* sl = a.slots + blockIdx.x;
@@ -2577,7 +2585,20 @@ __global__ __launch_bounds__(64, 1) void service_kernel(const gjkepa_svc_args a)
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h, 7) << 32);
             const double tol = __builtin_bit_cast(double, tb);
             const int ca = na < 0 || na > GJKEPA_MAX_HULL_VERTS ? 0 : na;
-            query_pair<double, double>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
+            const int nmax = na > nb ? na : nb;
+            if (!GJKEPA_SVC_LEAN) {
+                query_pair<double, double>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
+            } else if (na < 1 || nb < 1 || nmax > GJKEPA_SVC_MAX_HULL) {   // bad sizes / large hulls: declined
+                double o[13];
+#pragma unroll
+                for (int i = 0; i < 13; ++i) o[i] = 0.0;
+                store_record<64, double>(sl->rec, 0, grp.gl, o, 0, 0, GJKEPA_SVC_DECLINED, 0u);
+            } else if (nmax <= 64) {
+                query_pair_k<double, double, 1, double, true>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
+            } else {
+                static_assert(!GJKEPA_SVC_LEAN || GJKEPA_SVC_MAX_HULL <= 128, "the service's hull depth is two vertices per lane");
+                query_pair_k<double, double, 2, double, true>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
+            }
             __builtin_amdgcn_wave_barrier();
             GK_STAMP_END();
             const uint64_t t_done = wall_clock64();
@@ -2852,7 +2873,8 @@ extern "C" int gjkepa_diag_stamps(unsigned long long* out, int reset) {
 #endif
 
 hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStream_t s) {
-    using L_t = gk::QLds<double, double, GJKEPA_MAX_HULL_VERTS / 64>;
+    // the lean path's image (small polytope, K <= 2), or the full path's
+    using L_t = std::conditional_t<GJKEPA_SVC_LEAN != 0, gk::QLdsS<double, double, 2>, gk::QLds<double, double, GJKEPA_MAX_HULL_VERTS / 64>>;
     hipLaunchKernelGGL(gk::service_kernel, dim3((unsigned)n_slots), dim3(64), sizeof(L_t), s, a);
     return hipGetLastError();
 }

@@ -33,7 +33,7 @@ def main():
     c = torch.from_numpy(pool.hull_cnt).to(dev)
     p = torch.from_numpy(pool.pairs.reshape(-1).copy()).to(dev)
     out = torch.empty(n * 128, dtype=torch.uint8, device=dev)
-    wsb = gjkepa.workspace_bytes(n)
+    wsb = gjkepa.workspace_bytes_for(n, 0)          # 32-vertex hulls: no park slots
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     s = torch.cuda.Stream(dev)
 
