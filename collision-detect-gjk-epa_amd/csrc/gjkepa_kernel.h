@@ -391,7 +391,7 @@ hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s);
 // polytope outgrows the small one is declined (record status GJKEPA_SVC_DECLINED) and recomputed by
 // the caller on the combining path; larger hulls go there directly.  Records never differ.
 #ifndef GJKEPA_SVC_LEAN
-#define GJKEPA_SVC_LEAN 1        // 0: the full one-wave path (every hull size, restart with the large polytope; A/B)
+#define GJKEPA_SVC_LEAN 0        // 1: the lean path (A/B r5: lone call 46.7 vs 44.4 us, the declined pairs' combining round trips; no gain for a concurrent batch)
 #endif
 #ifndef GJKEPA_SVC_MAX_HULL
 #define GJKEPA_SVC_MAX_HULL (GJKEPA_SVC_LEAN ? 128 : GJKEPA_MAX_HULL_VERTS)
