@@ -508,7 +508,8 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
     int rc;
     if (GJKEPA_CONTACT_OVERLAP && n_pairs >= kOverlapMin && (rc = fork_state(s, &f))) return rc;
     const bool overlap = f != nullptr;
-    const bool e23 = overlap && e23_streams() == 2;      // EPA tiers 2 and 3 side by side
+    // EPA tiers 2 and 3 side by side (not when a contact pass forks after tier 3)
+    const bool e23 = overlap && e23_streams() == 2 && !((GJKEPA_FORK_MASK >> 3) & 1);
     const gjkepa_epa_args whole = a;                     // (a.pairs / route / out / n_pairs: a pair range below)
     int64_t r_first = 0;                                 // the pair range `a` points at
     auto range = [&](int64_t first, int64_t count) {     // point `a` at pairs [first, first + count)
@@ -632,7 +633,6 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
                     return hip_fail(e, "EPA tier 3 stream fork");
                 if ((rc = epa_tier(3, f->s3))) return rc;
                 if ((e = hipEventRecord(f->join23, f->s3)) != hipSuccess) return hip_fail(e, "EPA tier 3 stream join");
-                static_assert(!((GJKEPA_FORK_MASK >> 3) & 1), "no contact pass is forked after EPA tier 3");
             }
             if (e23 && t == 3) continue;                     // launched beside tier 2
             if (e23 && t == 4 && (e = hipStreamWaitEvent(s, f->join23, 0)) != hipSuccess)

@@ -38,6 +38,9 @@ def main():
     s = torch.cuda.Stream(dev)
 
     def rate(steps=20):
+        # chain_ms: each chain's own span on the GPU (its head event to its last kernel's end, from the
+        # library's launch timing), which excludes any gap while the host thread was still enqueueing it
+        gjkepa.launch_timing(True)
         with torch.cuda.stream(s):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t = time.perf_counter()
@@ -49,8 +52,12 @@ def main():
             e1.record(s)
             s.synchronize()
             wall = time.perf_counter() - t
+        gjkepa.launch_timing(False)
+        lt = gjkepa.launch_timing_read()
+        chain_ms = float(np.mean([lt["end_ms"][lt["chain"] == k].max() for k in set(lt["chain"].tolist())]))
         return {"M_per_s_events": round(n * steps / (e0.elapsed_time(e1) * 1e-3) / 1e6, 2),
-                "M_per_s_wall": round(n * steps / wall / 1e6, 2)}
+                "M_per_s_wall": round(n * steps / wall / 1e6, 2), "chain_ms": round(chain_ms, 4),
+                "M_per_s_chain": round(n / (chain_ms * 1e-3) / 1e6, 2)}
 
     rng = np.random.default_rng(3)
     qs = []
