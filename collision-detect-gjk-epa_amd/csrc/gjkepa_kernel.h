@@ -192,6 +192,12 @@
 #ifndef GJKEPA_CONTACT_META
 #define GJKEPA_CONTACT_META 1       // contact tiers load every routed pair's hull counts / offsets once per chunk (0: per pair, A/B)
 #endif
+#ifndef GJKEPA_E1_PRIO
+#define GJKEPA_E1_PRIO 0            // wave priority (s_setprio) of EPA tier 1's waves (0: default, A/B)
+#endif
+#ifndef GJKEPA_EPA_HPACK
+#define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B)
+#endif
 #ifndef GJKEPA_EPA_PLACE
 #define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
 #endif

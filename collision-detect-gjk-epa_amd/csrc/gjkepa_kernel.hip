@@ -46,6 +46,18 @@ constexpr int ST_REDO = 103;    // internal (fp32 compute): answer not certified
 constexpr int ST_PARKED = 104;  // internal: polytope parked for the next tier (gjkepa_kernel.h "Polytope parking")
 constexpr int ST_CASE04 = 105;  // internal: contact v2 case_04, left to the full contact pass (contact_kernel DEFER04)
 
+// A compiler-only memory fence (no instruction): LDS reads after it are not hoisted above it.  Without
+// it the scheduler issues a whole hull's K vertex loads (3K VGPRs in fp64: 6 per vertex) ahead of the
+// dot products, and for hull B while hull A's are still live, which is where most of the GJK / EPA
+// tiers' register peaks and scratch spills came from.
+DEV void gk_lds_fence() { asm volatile("" ::: "memory"); }
+#ifndef GJKEPA_SCREEN_FENCE
+#define GJKEPA_SCREEN_FENCE 0    // fence between hull A's and hull B's fp32-screened support scans
+#endif
+#ifndef GJKEPA_DOTS_FENCE_MIN_K
+#define GJKEPA_DOTS_FENCE_MIN_K 0   // support_dots: fence between the two hulls' reads in tiers with K >= this (0: none)
+#endif
+
 // fp32 certificate.  An fp32 EPA can build an invalid polytope from inconsistent visibility decisions
 // on near-coplanar faces (the fp32 rounding of a sliver's normal), after which its MINLOC distance
 // drops and it may stop far from the penetration depth (C5: 20% low, normal off by 0.4 rad on one
@@ -145,6 +157,13 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
     static constexpr int NHP = NH + GJKEPA_LDS_SKEW;
     static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 && !GJKEPA_EPA_PLACE ? G : 1;
     static constexpr int NC = ((VC_ == 0 && FC_ == 1) || FUSED) ? NH : 1;
+    // Horizon list packing (GJKEPA_EPA_HPACK): where every face key fits 16 bits (kbase grows by at
+    // most 3 FC per hull insertion, two insertions per iteration, <= 100 iterations), a horizon edge is
+    // one word u | w << 8 | key << 16 and the list holds FC / 2 edges (hull_add defers a pair whose
+    // horizon is longer, which a polytope of VC <= 64 vertices practically never has), so EPA tier 0's
+    // image fits a twelfth wave per CU.
+    static constexpr bool HPACK = GJKEPA_EPA_HPACK && VC_ > 0 && 4 + 600 * FC_ < 65536;
+    static constexpr int HC = HPACK ? FC / 2 : FC;
 #if GJKEPA_HULL_AOS
     HV<TH> hv[2][NH];                       // hull A (0) / B (1) vertex i, storage precision
 #else
@@ -159,13 +178,13 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
             union X {
                 struct H {                                                                 // hull_add lists
                     uint64_t visl[FC];                       // visible faces: ids | key << 32
-                    uint32_t horu[FC], hork[FC];             // horizon edges: u | w << 8, new face key
+                    uint32_t horu[HC], hork[HPACK ? 1 : FC]; // horizon edges: u | w << 8 (| new face key << 16 if HPACK), new face key
 #if !GJKEPA_EPA_PLACE
                     T sn[GS][4];                             // new faces of one round: normal, |distance|
                     uint32_t sv[GS], sk[GS];                 //   ids, key
 #endif
                 } h;
-                struct S { T cur[FC]; T srt[FC]; } s;                                     // sorted_equal
+                struct S { T srt[FC]; } s;                                                 // sorted_equal
                 struct O { uint32_t key[FC]; uint32_t ord[FC]; } o;                       // centroid order
             } x;
         } e;
@@ -308,6 +327,23 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
     T (&ta)[K] = D.t[0];
     T (&tb)[K] = D.t[1];
     T va = -Tol<T>::BIG, vb = -Tol<T>::BIG;
+    if constexpr (GJKEPA_DOTS_FENCE_MIN_K > 0 && K >= GJKEPA_DOTS_FENCE_MIN_K) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + c.g.gl;
+        const V3<T> a = c.AV(k);
+        ta[k] = i < c.na ? d.x * a.x + d.y * a.y + d.z * a.z : -Tol<T>::BIG;
+        va = ta[k] > va ? ta[k] : va;
+    }
+    gk_lds_fence();                      // hull B's vertices are read after hull A's dots
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = k * G + c.g.gl;
+        const V3<T> b = c.BV(k);
+        tb[k] = i < c.nb ? -(d.x * b.x + d.y * b.y + d.z * b.z) : -Tol<T>::BIG;
+        vb = tb[k] > vb ? tb[k] : vb;
+    }
+    } else {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
@@ -316,6 +352,7 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
         tb[k] = i < c.nb ? -(d.x * b.x + d.y * b.y + d.z * b.z) : -Tol<T>::BIG;
         va = ta[k] > va ? ta[k] : va;
         vb = tb[k] > vb ? tb[k] : vb;
+    }
     }
     va = gmax<G>(va);
     vb = gmax<G>(vb);
@@ -337,6 +374,9 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
 CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
     if constexpr (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) {
         screened_idx(c, d, 0, c.vmax_a, ia);
+#if GJKEPA_SCREEN_FENCE
+        gk_lds_fence();                  // hull B's screen reads its vertices after hull A's is done
+#endif
         screened_idx(c, d, 1, c.vmax_b, ib);
         return;
     }
@@ -454,6 +494,7 @@ template <typename T> DEV T qnan() { return __builtin_nan(""); }
 CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, int& nf, V3<T> p, bool append,
                        int kexist, bool& changed, bool save_eq) {
     constexpr int R = (FC + G - 1) / G;
+    using L_t = typename CTX::L_t;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
     uint64_t vm[R];
@@ -529,14 +570,17 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         const uint64_t m = c.g.ballot(hz);
         if (hz) {
             const int pos = nh + mbcnt(m);
-            if (pos < FC) { E.x.h.horu[pos] = uw; E.x.h.hork[pos] = nkey; }
+            if (pos < L_t::HC) {
+                if constexpr (L_t::HPACK) E.x.h.horu[pos] = uw | (nkey << 16);
+                else { E.x.h.horu[pos] = uw; E.x.h.hork[pos] = nkey; }
+            }
         }
         nh += popc(m);
     }
     nh = c.g.uni(nh);
     GK_STAMP(SE_HOR);
     const int nf2 = nf - nvis + nh;
-    if (nh > FC || nf2 > FC) return ST_DEFER;
+    if (nh > L_t::HC || nf2 > FC) return ST_DEFER;
     kbase += 3u * (uint32_t)nvis;
     if (save_eq && nf2 == nf) {
 #pragma unroll
@@ -573,7 +617,8 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             const V3<T> n = uninml(U, W, P);
             bad = bad || is_zero_nml(n);
             const T dd = dot(vsub(zero3<T>(), U), n);
-            const uint32_t fv = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16), kk = E.x.h.hork[h];
+            const uint32_t fv = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
+            const uint32_t kk = L_t::HPACK ? uw >> 16 : E.x.h.hork[h];
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (r == row) { F.nx[r] = n.x; F.ny[r] = n.y; F.nz[r] = n.z; F.d[r] = dd; F.fv[r] = fv; F.key[r] = kk; }
@@ -631,7 +676,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             E.x.h.sn[gl][0] = n.x; E.x.h.sn[gl][1] = n.y; E.x.h.sn[gl][2] = n.z;
             E.x.h.sn[gl][3] = dot(vsub(zero3<T>(), U), n);
             E.x.h.sv[gl] = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
-            E.x.h.sk[gl] = E.x.h.hork[h];
+            E.x.h.sk[gl] = L_t::HPACK ? uw >> 16 : E.x.h.hork[h];
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -759,26 +804,7 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F, int hw) {
     constexpr int R = (FC + G - 1) / G;
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int f = r * G + gl;
-        if (f < FC) E.x.s.cur[f] = (F.fv[r] & kEmpty) ? qnan<T>() : fabs(F.d[r]);
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = r * G + gl;
-        if (i < FC) {
-            const T x = E.x.s.cur[i];
-            if (x == x) {
-                int rk = 0;
-                for (int j = 0; j < hw; ++j) { const T y = E.x.s.cur[j]; rk += (y < x) || (y == x && j < i); }
-                E.x.s.srt[rk] = x;
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    bool ok = true;
+    // the saved list, sorted (rank among the saved values, ties by slot) into srt[]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int i = r * G + gl;
@@ -787,8 +813,28 @@ CTX_T DEV bool sorted_equal(CTX& c, const FACES_T& F, int hw) {
             if (x == x) {
                 int rk = 0;
                 for (int j = 0; j < hw; ++j) { const T y = E.dsv[j]; rk += (y < x) || (y == x && j < i); }
-                if (!(fabs(x - E.x.s.srt[rk]) < Tol<T>::PT)) ok = false;
+                E.x.s.srt[rk] = x;
             }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // dsv[] is read again only after the next save (hull_add / epa_grow save it in every iteration
+    // whose termination test compares it), so the current values are ranked in its place
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = r * G + gl;
+        if (f < FC) E.dsv[f] = (F.fv[r] & kEmpty) ? qnan<T>() : fabs(F.d[r]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * G + gl;
+        if (i < FC && !(F.fv[r] & kEmpty)) {
+            const T x = fabs(F.d[r]);
+            int rk = 0;
+            for (int j = 0; j < hw; ++j) { const T y = E.dsv[j]; rk += (y < x) || (y == x && j < i); }
+            if (!(fabs(x - E.x.s.srt[rk]) < Tol<T>::PT)) ok = false;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1446,6 +1492,116 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
     return 0;
 }
 
+// case_04 with the point sets left in LDS (GJKEPA_CASE04_LDS): the same arithmetic as contact_case04,
+// but each lane reads its set elements (sx/sy/sz[i]), the ordered polygon (sx[ord[q]]) and its next
+// vertex from the group's LDS image at each use instead of holding K-element copies in registers, so
+// the contact kernel does not carry 60 VGPRs for the quarter of its pairs that take case_04.
+CTX_T DEV int contact_case04_lds(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
+    auto& C = c.L.u.c;
+    const int gl = c.g.gl;
+    const T TWO_PI_SP = (T)(2.0f * 3.14159274101257324f);
+    auto pt = [&](int i) { return vmk<T>(C.sx[i], C.sy[i], C.sz[i]); };
+    // OVERLAP (:1399-1418): all points pairwise within 1e-12 -> order unchanged
+    bool diff = false;
+    for (int i0 = 0; i0 < na; i0 += G) {
+        int i = i0 + gl;
+        if (i < na) {
+            for (int j = 0; j < na; ++j)
+                diff = diff || fabs(C.sx[i] - C.sx[j]) > Tol<T>::Z || fabs(C.sy[i] - C.sy[j]) > Tol<T>::Z ||
+                       fabs(C.sz[i] - C.sz[j]) > Tol<T>::Z;
+        }
+    }
+    const bool ovl = !c.g.any(diff);
+    if (!ovl) {
+        T sx = 0, sy = 0, sz = 0;
+        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        const T dn = (T)na;
+        const V3<T> cen = vmk<T>(sx / dn, sy / dn, sz / dn);
+        const V3<T> p0 = pt(0);
+        const V3<T> nrm = cross(vsub(pt(1), p0), vsub(pt(2), p0));
+        V3<T> prev = p0;
+        if (gl == 0) C.ord[0] = 0u;
+        uint32_t used = 0;                                         // bit k: element k*G + gl is placed
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = k * G + gl;
+            if (i < na) { const V3<T> q = pt(i); if (q.x == p0.x && q.y == p0.y && q.z == p0.z) used |= 1u << k; }
+        }
+        for (int s = 1; s < na; ++s) {
+            gk_lds_fence();
+            T best = Tol<T>::BIG;
+            int bi = 0x7fffffff;
+#pragma unroll 1
+            for (int k = 0; k < K && k * G < na; ++k) {             // one atan2 / fmod instance, not K
+                const int j = k * G + gl;
+                if (j < na && !((used >> k) & 1u)) {
+                    const V3<T> w1 = vsub(pt(j), cen), w2 = vsub(prev, cen);
+                    T ang = tatan2(dot(nrm, cross(w2, w1)), dot(w1, w2));
+                    ang = tfmod(ang + TWO_PI_SP, TWO_PI_SP);
+                    if (ang < best) { best = ang; bi = j; }
+                }
+            }
+            gargmin<G>(best, bi);
+            bi = c.g.uni(bi);
+            if (bi == 0x7fffffff) return GJKEPA_STATUS_DEGENERATE;
+            prev = pt(bi);
+            if (gl == 0) C.ord[s] = (uint32_t)bi;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int j = k * G + gl;
+                if (j < na) { const V3<T> q = pt(j); if (q.x == prev.x && q.y == prev.y && q.z == prev.z) used |= 1u << k; }
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ordered polygon vertex q (SORT_CLOCK's order, or the input order when the points overlap)
+    auto opt = [&](int q) { return pt(ovl ? q : (int)C.ord[q]); };
+    // IS_INSIDE_PF(sorted polygon, b_t) for t = 0, 1: edge q = (vertex q, vertex q + 1 mod na)
+    int cnt_in = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const V3<T> P = t ? b1 : b0;
+        auto cp_xy = [&](int q) {
+            const V3<T> a = opt(q), b = opt(q == na - 1 ? 0 : q + 1);
+            T v = (b.x - a.x) * (P.y - a.y) - (b.y - a.y) * (P.x - a.x);
+            if (fabs(v) < Tol<T>::Z) v = T(0);
+            return v;
+        };
+        auto cp_xz = [&](int q) {
+            const V3<T> a = opt(q), b = opt(q == na - 1 ? 0 : q + 1);
+            return (b.x - a.x) * (P.z - a.z) - (b.z - a.z) * (P.x - a.x);
+        };
+        bool pos = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = k * G + gl;
+            if (q < na) pos = pos || cp_xy(q) > Tol<T>::POS;
+        }
+        const bool xz = !c.g.any(pos);
+        gk_lds_fence();
+        const T c0 = xz ? cp_xz(0) : cp_xy(0);                   // element 0's cross product, on every lane
+        bool neg = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = k * G + gl;
+            if (q < na) neg = neg || c0 * (xz ? cp_xz(q) : cp_xy(q)) < T(0);
+        }
+        if (!c.g.any(neg)) ++cnt_in;
+    }
+    if (cnt_in == 0) {                                             // case_04_1
+        T sx = 0, sy = 0, sz = 0;
+        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        const T dn = (T)na;
+        res = foot_pl(vmk<T>(sx / dn, sy / dn, sz / dn), b0, b1);
+    } else {
+        res = vscl(T(0.5), vadd(b0, b1));                          // case_04_2 / case_04_3
+    }
+    return 0;
+}
+#ifndef GJKEPA_CASE04_LDS
+#define GJKEPA_CASE04_LDS 1      // case_04 reads its point sets from LDS (0: register copies, A/B)
+#endif
+
 // get_collisionPoint_02 (:457-696).  DEFER04: case_04 (SORT_CLOCK + polygon containment, a quarter of
 // C2's hits) is not computed here: ST_CASE04 hands the pair to the full contact pass, so the common
 // kernel does not carry case_04's registers (contact_kernel).
@@ -1484,13 +1640,13 @@ DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
         const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 1, D, t2, true);
-        return contact_case04(c, n2, q0, q1, res);
+        return GJKEPA_CASE04_LDS ? contact_case04_lds(c, n2, q0, q1, res) : contact_case04(c, n2, q0, q1, res);
     } else if (n1 >= 3 && n2 == 2) {                               // case_04(SPT_p1, SPT_p2)
         band_set(c, 1, D, t2, true);
         const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 0, D, t1, true);
-        return contact_case04(c, n1, q0, q1, res);
+        return GJKEPA_CASE04_LDS ? contact_case04_lds(c, n1, q0, q1, res) : contact_case04(c, n1, q0, q1, res);
     } else if (n1 >= 3 && n2 >= 3) {                               // case_05
         band_set(c, 0, D, t1, true);
         T sx = 0, sy = 0, sz = 0;
@@ -1802,14 +1958,16 @@ DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
     support_dots(c, n, D, ia, ib);
     GK_STAMP(SE_NEAR);
     V3<T> pt = zero3<T>();
-    bool same_n = true;
+    // get_info_collisionType (:343) along the EPA normal depends only on these dots: taken before the
+    // contact point, so the dots are dead during case_04 (the contact kernel's register peak)
+    int type = (version == 1 || version == 2) ? collision_type(c, D, tol_ff) : 0;
     if (version == 1) st = contact_v1(c, n, D, pt);                       // :329-340
     else if (version == 2) st = contact_v2<DEFER04>(c, D, pt);
-    else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; same_n = false; }
+    else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; }
     else st = GJKEPA_STATUS_BAD_VERSION;
     GK_STAMP(SE_CONT);
     if (st) return st;
-    const int type = same_n ? collision_type(c, D, tol_ff) : collision_type(c, n, tol_ff);   // :343
+    if (version == 3) type = collision_type(c, n, tol_ff);             // along v3's replaced normal
     GK_STAMP(SE_TYPE);
     const V3<T> q1 = c.A(ia), q2 = c.B(ib);
     __builtin_amdgcn_wave_barrier();
@@ -2304,6 +2462,11 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel_refill(const gjkepa_epa_a
     GK_GUARD(3, a.route_code);
     GK_STAMP_BEGIN();
     if (tier_empty(a.tally, a.route_code)) return;
+#if GJKEPA_E1_PRIO
+    // EPA tier 1 serves the few polytopes that outgrew tier 0, restarted: on C2 it is the chain's tail,
+    // beside the contact passes, so its waves take the SIMD's issue first
+    if (a.route_code == GJKEPA_ROUTE_EPA0 + 1) __builtin_amdgcn_s_setprio(GJKEPA_E1_PRIO);
+#endif
     tally_begin();
     PairQueue q(a.route, a.n_pairs, tail_unit<G, (2 * NG > 8 ? 2 * NG : 8)>(a.n_pairs), a.route_code, a.ctr);
     Ctx<T, TIn, G, K, VC, FC, LH> c{L, grp};
