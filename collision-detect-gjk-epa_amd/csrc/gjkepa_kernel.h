@@ -59,7 +59,7 @@
 #define GJKEPA_E0_FCAP 64
 #endif
 #ifndef GJKEPA_E0_MINW
-#define GJKEPA_E0_MINW 3        // with GJKEPA_E0_LH: 160 VGPRs, no spills; LDS holds 11 waves/CU
+#define GJKEPA_E0_MINW 3        // with GJKEPA_E0_LH: 168 VGPRs; with GJKEPA_EPA_HPACK the LDS holds 12 waves/CU
 #endif
 #ifndef GJKEPA_E0_REFILL
 #define GJKEPA_E0_REFILL 2      // refill a wave's groups once this many are idle (0: per-round kernel)
@@ -162,7 +162,7 @@
 #define GJKEPA_C0_K 4
 #endif
 #ifndef GJKEPA_C0_MINW
-#define GJKEPA_C0_MINW 2
+#define GJKEPA_C0_MINW 3        // A/B r5 (2 rounds): C2 162.7 -> 163.6 M/s, C4 / C5 unchanged (LDS allows 10 waves/CU)
 #endif
 // contact tier 0's main pass leaves contact v2's case_04 (SORT_CLOCK and the polygon containment test,
 // about a quarter of C2's hits) to a full pass of the same hull shape (GJKEPA_CONTACT_C04) or to contact
@@ -193,10 +193,10 @@
 #define GJKEPA_CONTACT_META 1       // contact tiers load every routed pair's hull counts / offsets once per chunk (0: per pair, A/B)
 #endif
 #ifndef GJKEPA_E1_PRIO
-#define GJKEPA_E1_PRIO 0            // wave priority (s_setprio) of EPA tier 1's waves (0: default, A/B)
+#define GJKEPA_E1_PRIO 2            // wave priority (s_setprio) of EPA tier 1's waves (0: default; A/B r5: C2 +0.2%, C5 +0.6%)
 #endif
 #ifndef GJKEPA_EPA_HPACK
-#define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B)
+#define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B r5 C2 157.3 -> 162.7)
 #endif
 #ifndef GJKEPA_EPA_PLACE
 #define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
