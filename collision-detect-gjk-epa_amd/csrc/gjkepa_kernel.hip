@@ -189,7 +189,9 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
             } x;
         } e;
         struct Gh { T l1[12], l2[12]; } g;   // GJK simplex history (:193-194)
-        struct C { T sx[NC], sy[NC], sz[NC], pol[NC]; uint32_t ord[NC]; } c;   // contact features
+        // contact features: a point set (SPT) is a list of hull vertices, kept as vertex index | side << 15
+        // and read back from the hull image (the same fp32 -> T conversion as when it was selected)
+        struct C { T pol[NC]; uint32_t ord[NC]; uint16_t si[NC]; } c;
     } u;
 };
 
@@ -1270,6 +1272,13 @@ CTX_T DEV T hull_dot_max(CTX& c, int side, V3<T> n) {
     return gmax<G>(mx);
 }
 // members with dot(n,p) > mx - band (index order) -> LDS sx/sy/sz when `store`; returns count
+// element i of the contact point set: its hull vertex, converted as when it was selected
+CTX_T DEV V3<T> set_pt(const CTX& c, int i) {
+    const uint32_t w = c.L.u.c.si[i];
+    const V3<TH> v = c.raw((int)(w >> 15), (int)(w & 0x7fffu));
+    return vmk<T>((T)v.x, (T)v.y, (T)v.z);
+}
+
 CTX_T DEV int hull_band_set(CTX& c, int side, V3<T> n, T mx, T band, bool store) {
     int cnt = 0;
     auto& C = c.L.u.c;
@@ -1281,7 +1290,7 @@ CTX_T DEV int hull_band_set(CTX& c, int side, V3<T> n, T mx, T band, bool store)
         T t = n.x * px + n.y * py + n.z * pz;
         bool in = i < (side ? c.nb : c.na) && t > mx - band;
         uint64_t m = c.g.ballot(in);
-        if (store && in) { int pos = cnt + mbcnt(m); C.sx[pos] = px; C.sy[pos] = py; C.sz[pos] = pz; }
+        if (store && in) { int pos = cnt + mbcnt(m); C.si[pos] = (uint16_t)(i | (side << 15)); }
         cnt += popc(m);
     }
     __builtin_amdgcn_wave_barrier();
@@ -1298,9 +1307,8 @@ CTX_T DEV int band_set(CTX& c, int side, const DotSet<T, K>& D, T thr, bool stor
         const bool in = i < (side ? c.nb : c.na) && D.t[side][k] > thr;
         const uint64_t m = c.g.ballot(in);
         if (store && in) {
-            const V3<T> p = side ? c.BV(k) : c.AV(k);
             const int pos = cnt + mbcnt(m);
-            C.sx[pos] = p.x; C.sy[pos] = p.y; C.sz[pos] = p.z;
+            C.si[pos] = (uint16_t)(i | (side << 15));
         }
         cnt += popc(m);
     }
@@ -1337,7 +1345,7 @@ CTX_T DEV int contact_v1(CTX& c, V3<T> n, const DotSet<T, K>& D, V3<T>& res) {
     if (a0 != a1 && b0 != b1) {
         const int C = band_set(c, 0, D, D.m[0] - T(0.1), true);
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < C; ++i) { sx += c.L.u.c.sx[i]; sy += c.L.u.c.sy[i]; sz += c.L.u.c.sz[i]; }
+        for (int i = 0; i < C; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dc = (T)C;
         res = vmk<T>(sx / dc, sy / dc, sz / dc);
     }
@@ -1377,9 +1385,11 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
     for (int i0 = 0; i0 < na; i0 += G) {
         int i = i0 + gl;
         if (i < na) {
-            for (int j = 0; j < na; ++j)
-                diff = diff || fabs(C.sx[i] - C.sx[j]) > Tol<T>::Z || fabs(C.sy[i] - C.sy[j]) > Tol<T>::Z ||
-                       fabs(C.sz[i] - C.sz[j]) > Tol<T>::Z;
+            const V3<T> pi = set_pt(c, i);
+            for (int j = 0; j < na; ++j) {
+                const V3<T> pj = set_pt(c, j);
+                diff = diff || fabs(pi.x - pj.x) > Tol<T>::Z || fabs(pi.y - pj.y) > Tol<T>::Z || fabs(pi.z - pj.z) > Tol<T>::Z;
+            }
         }
     }
     const bool ovl = !c.g.any(diff);
@@ -1388,16 +1398,17 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         int i = k * G + gl;
-        px[k] = i < na ? C.sx[i] : T(0); py[k] = i < na ? C.sy[i] : T(0); pz[k] = i < na ? C.sz[i] : T(0);
+        const V3<T> q = set_pt(c, i < na ? i : 0);
+        px[k] = q.x; py[k] = q.y; pz[k] = q.z;
         used[k] = false;
     }
     if (!ovl) {
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        for (int i = 0; i < na; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dn = (T)na;
         const V3<T> cen = vmk<T>(sx / dn, sy / dn, sz / dn);
-        const V3<T> p0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
-        const V3<T> nrm = cross(vsub(vmk<T>(C.sx[1], C.sy[1], C.sz[1]), p0), vsub(vmk<T>(C.sx[2], C.sy[2], C.sz[2]), p0));
+        const V3<T> p0 = set_pt(c, 0);
+        const V3<T> nrm = cross(vsub(set_pt(c, 1), p0), vsub(set_pt(c, 2), p0));
         V3<T> prev = p0;
         if (gl == 0) C.ord[0] = 0u;
 #pragma unroll
@@ -1421,7 +1432,7 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
             gargmin<G>(best, bi);
             bi = c.g.uni(bi);
             if (bi == 0x7fffffff) return GJKEPA_STATUS_DEGENERATE;
-            prev = vmk<T>(C.sx[bi], C.sy[bi], C.sz[bi]);
+            prev = set_pt(c, bi);
             if (gl == 0) C.ord[s] = (uint32_t)bi;
 #pragma unroll
             for (int k = 0; k < K; ++k) used[k] = used[k] || (px[k] == prev.x && py[k] == prev.y && pz[k] == prev.z);
@@ -1430,7 +1441,7 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             int q = k * G + gl;
-            if (q < na) { int src = (int)C.ord[q]; px[k] = C.sx[src]; py[k] = C.sy[src]; pz[k] = C.sz[src]; }
+            if (q < na) { const V3<T> p = set_pt(c, (int)C.ord[q]); px[k] = p.x; py[k] = p.y; pz[k] = p.z; }
         }
     }
     // next polygon vertex of each lane's element, through the pol[] exchange
@@ -1483,7 +1494,7 @@ CTX_T DEV int contact_case04(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res) {
     }
     if (cnt_in == 0) {                                             // case_04_1
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        for (int i = 0; i < na; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dn = (T)na;
         res = foot_pl(vmk<T>(sx / dn, sy / dn, sz / dn), b0, b1);
     } else {
@@ -1500,21 +1511,23 @@ CTX_T DEV int contact_case04_lds(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res)
     auto& C = c.L.u.c;
     const int gl = c.g.gl;
     const T TWO_PI_SP = (T)(2.0f * 3.14159274101257324f);
-    auto pt = [&](int i) { return vmk<T>(C.sx[i], C.sy[i], C.sz[i]); };
+    auto pt = [&](int i) { return set_pt(c, i); };
     // OVERLAP (:1399-1418): all points pairwise within 1e-12 -> order unchanged
     bool diff = false;
     for (int i0 = 0; i0 < na; i0 += G) {
         int i = i0 + gl;
         if (i < na) {
-            for (int j = 0; j < na; ++j)
-                diff = diff || fabs(C.sx[i] - C.sx[j]) > Tol<T>::Z || fabs(C.sy[i] - C.sy[j]) > Tol<T>::Z ||
-                       fabs(C.sz[i] - C.sz[j]) > Tol<T>::Z;
+            const V3<T> pi = set_pt(c, i);
+            for (int j = 0; j < na; ++j) {
+                const V3<T> pj = set_pt(c, j);
+                diff = diff || fabs(pi.x - pj.x) > Tol<T>::Z || fabs(pi.y - pj.y) > Tol<T>::Z || fabs(pi.z - pj.z) > Tol<T>::Z;
+            }
         }
     }
     const bool ovl = !c.g.any(diff);
     if (!ovl) {
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        for (int i = 0; i < na; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dn = (T)na;
         const V3<T> cen = vmk<T>(sx / dn, sy / dn, sz / dn);
         const V3<T> p0 = pt(0);
@@ -1590,7 +1603,7 @@ CTX_T DEV int contact_case04_lds(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res)
     }
     if (cnt_in == 0) {                                             // case_04_1
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < na; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        for (int i = 0; i < na; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dn = (T)na;
         res = foot_pl(vmk<T>(sx / dn, sy / dn, sz / dn), b0, b1);
     } else {
@@ -1615,42 +1628,42 @@ DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
     res = zero3<T>();
     if (n1 == 1 && n2 == 1) {                                      // case_01
         band_set(c, 0, D, t1, true);
-        const V3<T> a = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
+        const V3<T> a = set_pt(c, 0);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 1, D, t2, true);
-        res = vdiv(vadd(a, vmk<T>(C.sx[0], C.sy[0], C.sz[0])), T(2));
+        res = vdiv(vadd(a, set_pt(c, 0)), T(2));
     } else if (n1 == 1 && n2 >= 2) {                               // case_02
         band_set(c, 0, D, t1, true);
-        res = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
+        res = set_pt(c, 0);
     } else if (n1 >= 2 && n2 == 1) {
         band_set(c, 1, D, t2, true);
-        res = vmk<T>(C.sx[0], C.sy[0], C.sz[0]);
+        res = set_pt(c, 0);
     } else if (n1 == 2 && n2 == 2) {                               // case_03
         band_set(c, 0, D, t1, true);
-        const V3<T> a0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), a1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
+        const V3<T> a0 = set_pt(c, 0), a1 = set_pt(c, 1);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 1, D, t2, true);
         V3<T> f1, f2;
-        foot_ll(a0, a1, vmk<T>(C.sx[0], C.sy[0], C.sz[0]), vmk<T>(C.sx[1], C.sy[1], C.sz[1]), f1, f2);
+        foot_ll(a0, a1, set_pt(c, 0), set_pt(c, 1), f1, f2);
         res = vdiv(vadd(f1, f2), T(2));
     } else if (DEFER04 && ((n1 == 2 && n2 >= 3) || (n1 >= 3 && n2 == 2))) {
         return ST_CASE04;
     } else if (n1 == 2 && n2 >= 3) {                               // case_04(SPT_p2, SPT_p1)
         band_set(c, 0, D, t1, true);
-        const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
+        const V3<T> q0 = set_pt(c, 0), q1 = set_pt(c, 1);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 1, D, t2, true);
         return GJKEPA_CASE04_LDS ? contact_case04_lds(c, n2, q0, q1, res) : contact_case04(c, n2, q0, q1, res);
     } else if (n1 >= 3 && n2 == 2) {                               // case_04(SPT_p1, SPT_p2)
         band_set(c, 1, D, t2, true);
-        const V3<T> q0 = vmk<T>(C.sx[0], C.sy[0], C.sz[0]), q1 = vmk<T>(C.sx[1], C.sy[1], C.sz[1]);
+        const V3<T> q0 = set_pt(c, 0), q1 = set_pt(c, 1);
         __builtin_amdgcn_wave_barrier();
         band_set(c, 0, D, t1, true);
         return GJKEPA_CASE04_LDS ? contact_case04_lds(c, n1, q0, q1, res) : contact_case04(c, n1, q0, q1, res);
     } else if (n1 >= 3 && n2 >= 3) {                               // case_05
         band_set(c, 0, D, t1, true);
         T sx = 0, sy = 0, sz = 0;
-        for (int i = 0; i < n1; ++i) { sx += C.sx[i]; sy += C.sy[i]; sz += C.sz[i]; }
+        for (int i = 0; i < n1; ++i) { const V3<T> q = set_pt(c, i); sx += q.x; sy += q.y; sz += q.z; }
         const T dn = (T)n1;
         res = vmk<T>(sx / dn, sy / dn, sz / dn);
     } else {
