@@ -181,7 +181,7 @@
 #define GJKEPA_C1_K 4
 #endif
 #ifndef GJKEPA_C1_MINW
-#define GJKEPA_C1_MINW 2        // keeps the LDS-hull contact tier at <= 256 VGPRs (2 waves/SIMD)
+#define GJKEPA_C1_MINW 3        // A/B r5 (2 rounds): 2 -> 3 waves/SIMD C4 39.9 -> 40.6, C5 23.1 -> 23.5 M/s, C2 unchanged
 #endif
 #ifndef GJKEPA_EPA_SEED
 #define GJKEPA_EPA_SEED 1           // refill tiers: a fresh pair's iteration 1 joins the common support step (epa_seed)

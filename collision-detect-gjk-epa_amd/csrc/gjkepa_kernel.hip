@@ -157,12 +157,16 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
     static constexpr int NHP = NH + GJKEPA_LDS_SKEW;
     static constexpr int VC = VC_ > 0 ? VC_ : 1, FC = VC_ > 0 ? FC_ : 1, GS = VC_ > 0 && !GJKEPA_EPA_PLACE ? G : 1;
     static constexpr int NC = ((VC_ == 0 && FC_ == 1) || FUSED) ? NH : 1;
-    // Horizon list packing (GJKEPA_EPA_HPACK): where every face key fits 16 bits (kbase grows by at
-    // most 3 FC per hull insertion, two insertions per iteration, <= 100 iterations), a horizon edge is
-    // one word u | w << 8 | key << 16 and the list holds FC / 2 edges (hull_add defers a pair whose
-    // horizon is longer, which a polytope of VC <= 64 vertices practically never has), so EPA tier 0's
-    // image fits a twelfth wave per CU.
-    static constexpr bool HPACK = GJKEPA_EPA_HPACK && VC_ > 0 && 4 + 600 * FC_ < 65536;
+    // Horizon list packing (GJKEPA_EPA_HPACK): a horizon edge is one word u | w << HVB | key << 2 HVB
+    // (HVB bits per vertex id) where every face key fits the rest (kbase grows by at most 3 FC per hull
+    // insertion, two insertions per iteration, <= 100 iterations), and the list holds FC / 2 edges
+    // (hull_add defers a pair whose horizon is longer: at most VC edges, so only tiers with VC > FC / 2
+    // can, and a 33-edge horizon on a polytope of at most 40 vertices is not seen).  EPA tiers 0 and 4
+    // then fit a twelfth wave per CU.  Tiers whose polytopes are larger than that and whose occupancy
+    // is set by registers (1 and 2, 72 / 128) keep the two-word list: packed, C5 lost 0.9%.
+    static constexpr int HVB = VC_ <= 128 ? 7 : 8;
+    static constexpr bool HPACK = GJKEPA_EPA_HPACK && VC_ > 0 && VC_ <= (1 << HVB) && (VC_ <= 40 || 2 * VC_ <= FC_) &&
+                                  4 + 600LL * FC_ < (1LL << (32 - 2 * HVB));
     static constexpr int HC = HPACK ? FC / 2 : FC;
 #if GJKEPA_HULL_AOS
     HV<TH> hv[2][NH];                       // hull A (0) / B (1) vertex i, storage precision
@@ -566,14 +570,14 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
                 rank += (uint32_t)(qj >> 32) < kk;
             }
             hz = !twin;
-            uw = u | (w << 8);
+            uw = u | (w << L_t::HVB);
             nkey = kbase + 3u * (uint32_t)rank + (uint32_t)s;
         }
         const uint64_t m = c.g.ballot(hz);
         if (hz) {
             const int pos = nh + mbcnt(m);
             if (pos < L_t::HC) {
-                if constexpr (L_t::HPACK) E.x.h.horu[pos] = uw | (nkey << 16);
+                if constexpr (L_t::HPACK) E.x.h.horu[pos] = uw | (nkey << (2 * L_t::HVB));
                 else { E.x.h.horu[pos] = uw; E.x.h.hork[pos] = nkey; }
             }
         }
@@ -614,13 +618,14 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         const int h = placed + mbcnt(fl);
         if (row >= 0 && h < nh) {
             const uint32_t uw = E.x.h.horu[h];
-            const int u = (int)(uw & 0xffu), w = (int)((uw >> 8) & 0xffu);
+            constexpr uint32_t vm_ = (1u << L_t::HVB) - 1u;
+            const int u = (int)(uw & vm_), w = (int)((uw >> L_t::HVB) & vm_);
             const V3<T> U = c.vert(u), W = c.vert(w);
             const V3<T> n = uninml(U, W, P);
             bad = bad || is_zero_nml(n);
             const T dd = dot(vsub(zero3<T>(), U), n);
             const uint32_t fv = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
-            const uint32_t kk = L_t::HPACK ? uw >> 16 : E.x.h.hork[h];
+            const uint32_t kk = L_t::HPACK ? uw >> (2 * L_t::HVB) : E.x.h.hork[h];
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (r == row) { F.nx[r] = n.x; F.ny[r] = n.y; F.nz[r] = n.z; F.d[r] = dd; F.fv[r] = fv; F.key[r] = kk; }
@@ -671,14 +676,15 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         const int h = h0 + gl;
         if (h < nh) {
             const uint32_t uw = E.x.h.horu[h];
-            const int u = (int)(uw & 0xffu), w = (int)((uw >> 8) & 0xffu);
+            constexpr uint32_t vm_ = (1u << L_t::HVB) - 1u;
+            const int u = (int)(uw & vm_), w = (int)((uw >> L_t::HVB) & vm_);
             const V3<T> U = c.vert(u), W = c.vert(w);
             const V3<T> n = uninml(U, W, P);
             bad = bad || is_zero_nml(n);
             E.x.h.sn[gl][0] = n.x; E.x.h.sn[gl][1] = n.y; E.x.h.sn[gl][2] = n.z;
             E.x.h.sn[gl][3] = dot(vsub(zero3<T>(), U), n);
             E.x.h.sv[gl] = (uint32_t)u | ((uint32_t)w << 8) | ((uint32_t)k << 16);
-            E.x.h.sk[gl] = L_t::HPACK ? uw >> 16 : E.x.h.hork[h];
+            E.x.h.sk[gl] = L_t::HPACK ? uw >> (2 * L_t::HVB) : E.x.h.hork[h];
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
