@@ -173,8 +173,8 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
 #else
     TH hx[2][NHP], hy[2][NHP], hz[2][NHP];  // hull A (0) / B (1) vertices, storage precision
 #endif
-    union U {
-        struct E {                       // EPA polytope (faces themselves are in registers)
+    struct None {};
+    struct E {                           // EPA polytope (faces themselves are in registers)
             T vx[VC], vy[VC], vz[VC];    // vertices by id
             T dsv[FC];                   // saved face distances by slot (termination test), NaN = none
             T best[3];                   // MINLOC face broadcast: normal, first vertex id
@@ -191,16 +191,19 @@ template <typename T, typename TH, int G, int K, int VC_, int FC_, bool FUSED = 
                 struct S { T srt[FC]; } s;                                                 // sorted_equal
                 struct O { uint32_t key[FC]; uint32_t ord[FC]; } o;                       // centroid order
             } x;
-        } e;
-        struct Gh { T l1[12], l2[12]; } g;   // GJK simplex history (:193-194)
-        // contact features: a point set (SPT) is a list of hull vertices, kept as vertex index | side << 15
-        // and read back from the hull image (the same fp32 -> T conversion as when it was selected)
-        struct C { T pol[NC]; uint32_t ord[NC]; uint16_t si[NC]; } c;
+    };
+    // contact features: a point set (SPT) is a list of hull vertices, kept as vertex index | side << 15
+    // and read back from the hull image (the same fp32 -> T conversion as when it was selected)
+    struct C { T pol[NC]; uint32_t ord[NC]; uint16_t si[NC]; };
+    // the GJK tiers (VC_ = FC_ = 0) carry nothing but the hulls, so GJK tier 0's 16 images fit 12 waves/CU
+    union U {
+        std::conditional_t<(VC_ > 0), E, None> e;
+        std::conditional_t<(VC_ > 0 || FC_ > 0), C, None> c;
     } u;
 };
 
 // Byte distance between the LDS images of consecutive groups of a wave.  The images of the groups
-// that share a 32-lane half (the unit ds_read/ds_write banks over) are skewed by G dwords modulo
+// that share a 32-lane half (the unit ds_read/ds_write banks over) are skewed by an odd multiple of G dwords modulo
 // the 32 four-byte banks, so group g's lane l and group g+1's lane l, touching the same field, hit
 // different banks; an unpadded image size is often a multiple of 16 or 32 dwords, which puts every
 // group of a half on the same banks (GJK tier 0: 16 groups, 8 per half, two distinct bank offsets).
@@ -215,8 +218,8 @@ template <typename L_t, int G> constexpr size_t lds_stride() {
         return dw * 4;
     } else {
         size_t dw = (sizeof(L_t) + 7) / 8 * 2;              // 8-byte aligned, in dwords
-        if (GJKEPA_LDS_SKEW && G < 32)
-            while (dw % 32 != (size_t)G) dw += 2;
+        if (GJKEPA_LDS_SKEW && G < 32)                      // dw = G x odd (mod 32): the 32 / G groups
+            while ((dw % 32) % G != 0 || ((dw % 32) / G) % 2 == 0) dw += 2;   // of a half on distinct banks
         return dw * 4;
     }
 }
@@ -1798,9 +1801,11 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
     bool axis_sep = false;
     {   // RoughCollisionDetection_SphericalEnvelope (:1165-1188)
         // the six sequential coordinate sums run on group lanes (sum j on lane j % G: hull j/3, axis j%3)
+        T cs[(6 + G - 1) / G];           // centroid coordinate j0 + gl of pass j0 / G (hull j / 3, axis j % 3)
 #pragma unroll
         for (int j0 = 0; j0 < 6; j0 += G) {
             const int j = j0 + gl;
+            cs[j0 / G] = T(0);
             if (j < 6) {
                 const int h = j / 3, ax = j - 3 * (j / 3);
 #if GJKEPA_HULL_AOS
@@ -1821,12 +1826,13 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
                     for (int u = 0; u < 8; ++u) sum += (T)v[u];
                 }
                 for (; i < n; ++i) sum += (T)col[CS * i];
-                L.u.g.l1[j] = sum / (T)n;
+                cs[j0 / G] = sum / (T)n;
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        const V3<T> m1 = vmk<T>(L.u.g.l1[0], L.u.g.l1[1], L.u.g.l1[2]), m2 = vmk<T>(L.u.g.l1[3], L.u.g.l1[4], L.u.g.l1[5]);
-        __builtin_amdgcn_wave_barrier();
+        // broadcast to the group from the lane that summed it (no LDS image space)
+        const int gb = c.g.lane & ~(G - 1);
+        auto mc = [&](int j) { return __shfl(cs[j / G], gb + j % G); };
+        const V3<T> m1 = vmk<T>(mc(0), mc(1), mc(2)), m2 = vmk<T>(mc(3), mc(4), mc(5));
         // max_i NORM2(p_i - m) = sqrt(max_i |p_i - m|^2): sqrt is monotone under correct rounding
         T r1 = -Tol<T>::BIG, r2 = -Tol<T>::BIG;
 #pragma unroll
