@@ -195,6 +195,9 @@
 #ifndef GJKEPA_E1_PRIO
 #define GJKEPA_E1_PRIO 2            // wave priority (s_setprio) of EPA tier 1's waves (0: default; A/B r5: C2 +0.2%, C5 +0.6%)
 #endif
+#ifndef GJKEPA_ARGMIN_SHFL
+#define GJKEPA_ARGMIN_SHFL 0        // EPA MINLOC face broadcast by ds_bpermute in groups below 32 lanes (0: LDS slot, A/B)
+#endif
 #ifndef GJKEPA_EPA_HPACK
 #define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B r5 C2 157.3 -> 162.7)
 #endif

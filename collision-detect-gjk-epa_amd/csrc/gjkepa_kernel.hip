@@ -791,6 +791,23 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& ne
         const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
         m = c.g.ballot(tie && kk == kmin);
     }
+    if constexpr (GJKEPA_ARGMIN_SHFL && G < 32) {
+        // the winner's row, selected on every lane, then pulled from the winner lane with ds_bpermute:
+        // no LDS slot write / read round trip (groups of 32 and 64 lanes keep the slot: a v_readlane
+        // broadcast lost there, round 3)
+        T bx = 0, by = 0, bz = 0;
+        uint32_t bw = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (rr == r) { bx = F.nx[r]; by = F.ny[r]; bz = F.nz[r]; bw = (F.fv[r] & 0xffu) | (F.d[r] < T(0) ? 0x80000000u : 0u); }
+        const int src = m ? (int)__builtin_ctzll(m) : c.g.lane;     // m: absolute lane bits of this group
+        dmin = vmin;
+        n = vmk<T>(__shfl(bx, src), __shfl(by, src), __shfl(bz, src));
+        const uint32_t bv = (uint32_t)__shfl((int)bw, src);
+        neg = (bv >> 31) != 0;
+        av = (int)(bv & 0xffu);
+        return;
+    }
     if (c.g.bit(m)) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
