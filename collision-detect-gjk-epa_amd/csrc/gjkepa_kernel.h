@@ -198,6 +198,9 @@
 #ifndef GJKEPA_ARGMIN_SHFL
 #define GJKEPA_ARGMIN_SHFL 0        // EPA MINLOC face broadcast by ds_bpermute in groups below 32 lanes (0: LDS slot, A/B)
 #endif
+#ifndef GJKEPA_HORIZON_W16
+#define GJKEPA_HORIZON_W16 1        // horizon twin test on 16-bit edge windows (0: byte compares; A/B r5: C2 +0.6%, C4 +1.6%, C5 +2.2%)
+#endif
 #ifndef GJKEPA_EPA_HPACK
 #define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B r5 C2 157.3 -> 162.7)
 #endif

@@ -541,7 +541,10 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             if (!live[r]) continue;
             if (c.g.bit(vm[r])) {
                 vp[r] = base + mbcnt(vm[r]);
-                E.x.h.visl[vp[r]] = (uint64_t)F.fv[r] | ((uint64_t)F.key[r] << 32);
+                // GJKEPA_HORIZON_W16: v0 repeated in byte 3, so the face's three directed edges are
+                // the 16-bit windows at bytes 0, 1 and 2 (v0v1, v1v2, v2v0)
+                const uint32_t fw = GJKEPA_HORIZON_W16 ? F.fv[r] | ((F.fv[r] & 0xffu) << 24) : F.fv[r];
+                E.x.h.visl[vp[r]] = (uint64_t)fw | ((uint64_t)F.key[r] << 32);
             }
             base += popc(vm[r]);
         }
@@ -565,12 +568,23 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             const uint32_t w = (fv >> (8 * (s == 2 ? 0 : s + 1))) & 0xffu;
             bool twin = false;
             int rank = 0;
-            for (int j = 0; j < nvis; ++j) {
-                const uint64_t qj = E.x.h.visl[j];
-                const uint32_t q = (uint32_t)qj;
-                const uint32_t q0 = q & 0xffu, q1 = (q >> 8) & 0xffu, q2 = (q >> 16) & 0xffu;
-                twin = twin || (q0 == w && q1 == u) || (q1 == w && q2 == u) || (q2 == w && q0 == u);
-                rank += (uint32_t)(qj >> 32) < kk;
+            if constexpr (GJKEPA_HORIZON_W16) {
+                // the twin (w, u) is a directed edge of face j iff it is one of its three 16-bit windows
+                const uint32_t t = w | (u << 8);
+                for (int j = 0; j < nvis; ++j) {
+                    const uint64_t qj = E.x.h.visl[j];
+                    const uint32_t q = (uint32_t)qj;
+                    twin = twin || (q & 0xffffu) == t || ((q >> 8) & 0xffffu) == t || (q >> 16) == t;
+                    rank += (uint32_t)(qj >> 32) < kk;
+                }
+            } else {
+                for (int j = 0; j < nvis; ++j) {
+                    const uint64_t qj = E.x.h.visl[j];
+                    const uint32_t q = (uint32_t)qj;
+                    const uint32_t q0 = q & 0xffu, q1 = (q >> 8) & 0xffu, q2 = (q >> 16) & 0xffu;
+                    twin = twin || (q0 == w && q1 == u) || (q1 == w && q2 == u) || (q2 == w && q0 == u);
+                    rank += (uint32_t)(qj >> 32) < kk;
+                }
             }
             hz = !twin;
             uw = u | (w << L_t::HVB);
