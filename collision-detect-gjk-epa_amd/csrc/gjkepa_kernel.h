@@ -201,6 +201,9 @@
 #ifndef GJKEPA_HORIZON_W16
 #define GJKEPA_HORIZON_W16 1        // horizon twin test on 16-bit edge windows (0: byte compares; A/B r5: C2 +0.6%, C4 +1.6%, C5 +2.2%)
 #endif
+#ifndef GJKEPA_SCREEN_SINGLE
+#define GJKEPA_SCREEN_SINGLE 1      // fp32 support screen: a group's single candidate is the answer, no fp64 dot (A/B r5: C4 +1.0%, C2 +0.2%)
+#endif
 #ifndef GJKEPA_EPA_HPACK
 #define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B r5 C2 157.3 -> 162.7)
 #endif

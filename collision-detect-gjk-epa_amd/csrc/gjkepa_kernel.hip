@@ -311,6 +311,16 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
         const int i = k * G + c.g.gl;
         if (i < n && !(sv[k] < thr)) cand |= 1u << k;      // NaN threshold or value: candidate
     }
+    if constexpr (GJKEPA_SCREEN_SINGLE) {
+        // one candidate in the whole group (the usual case): it is the fp64 argmax, so its index is
+        // the answer without its fp64 dot or the fp64 group reduction (an int group min only)
+        const uint64_t lanes = c.g.ballot(cand != 0);
+        if (!c.g.any(__builtin_popcount(cand) > 1) && popc(lanes) <= 1) {
+            const int key = gmin<G>(cand ? (int)__builtin_ctz(cand) * G + c.g.gl : 0x7FFFFFFF);
+            out = c.g.uni(key == 0x7FFFFFFF ? 0 : key);
+            return;
+        }
+    }
     T best = -Tol<T>::BIG;
     int bi = 0x7FFFFFFF;
     while (cand) {                                          // this lane's candidates in index order
