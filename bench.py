@@ -76,7 +76,7 @@ def moved_copy(pool, delta: float, seed: int) -> np.ndarray:
     return v.astype(pool.verts.dtype)
 
 
-WS_COUNTERS, WS_TALLY = 40, 48          # gjkepa_kernel.h: workspace header (uint32 words)
+WS_COUNTERS, WS_TALLY = gjkepa.WS_COUNTERS, gjkepa.WS_TALLY     # workspace header (uint32 words)
 ROUTE_EPA0, ROUTE_CT0 = 0x10, 0x20
 
 

@@ -301,15 +301,12 @@ int epa2_parts() {
     static const int p = parts_env("GJKEPA_EPA2_PARTS", GJKEPA_EPA2_PARTS);
     return p;
 }
-// launches of a contact pass with `tiers` contact tiers: a one-tier pass adds the case_04 pass its main
-// launch defers to (GJKEPA_C0_DEFER04; with two tiers, contact tier 1 takes those pairs)
-constexpr int contact_launches(int tiers) { return tiers == 1 && GJKEPA_C0_DEFER04 ? 2 : tiers; }
 // launches of an overlapped chain: 2 GJK + the EPA tiers (tiers 0 and 2 in up to kPartsMax parts) +
 // each fork point's contact pass (once per part); every launch owns one workspace counter
 constexpr int overlap_launches() {
     int n = GJKEPA_GJK_TIERS + GJKEPA_EPA_TIERS + 2 * (kPartsMax - 1);
     for (int t = 0; t < GJKEPA_EPA_TIERS; ++t)
-        if ((GJKEPA_FORK_MASK >> t) & 1) n += contact_launches(fork_contact_tiers(t)) * (t == 0 || t == 2 ? kPartsMax : 1);
+        if ((GJKEPA_FORK_MASK >> t) & 1) n += fork_contact_tiers(t) * (t == 0 || t == 2 ? kPartsMax : 1);
     return n;
 }
 static_assert(overlap_launches() + 1 <= GJKEPA_WS_COUNTERS, "workspace launch counters (+1: the fp32 redo launch)");
@@ -551,17 +548,6 @@ int enqueue(int32_t version, double tol_ff, int32_t vert_dtype, int32_t precisio
                                   [&] { return gjkepa_launch_contact(t, vert_dtype, precision, a, cs); });
             if (er != hipSuccess) return hip_fail(er, "contact tier launch");
         }
-        if (ntiers == 1 && GJKEPA_C0_DEFER04) {           // the case_04 pairs contact tier 0 left: base + 1
-            a.route_code = base + 1;
-            a.next_code = -1;
-            a.ctr = ctr + launch++;
-            a.claim = single ? 1 : kSparseClaim;
-            a.grid = 0;
-            a.guard = gjkepa_guard_of(a);
-            hipError_t er = timed("contact", GJKEPA_CONTACT_C04, part, a.route_code, r_first, a.n_pairs, cs,
-                                  [&] { return gjkepa_launch_contact(GJKEPA_CONTACT_C04, vert_dtype, precision, a, cs); });
-            if (er != hipSuccess) return hip_fail(er, "contact case_04 pass launch");
-        }
         return 0;
     };
     // fp32 compute: the pairs whose fp32 answer was not certified, recomputed in fp64 (after every
@@ -754,7 +740,7 @@ const char* gjkepa_version_string(void) {
     std::snprintf(buf, sizeof(buf),
                   "gjkepa-mi355x gfx950 wave64; GJK tiers G/K = %d/%d, %d/%d, %d/%d; EPA tiers G/K/VCAP/FCAP = "
                   "%d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d, %d/%d/%d/%d; contact tiers G/K = %d/%d, %d/%d; "
-                  "waves/SIMD G%d%d%d E%d%d%d%d%d%d C%d%d%d; LDS-hull G%d%d%d E%d%d%d%d%d%d C%d%d; "
+                  "waves/SIMD G%d%d%d E%d%d%d%d%d%d C%d%d; LDS-hull G%d%d%d E%d%d%d%d%d%d C%d%d; "
                   "-O3 -ffp-contract=off; src %s",
                   GJKEPA_G0_G, GJKEPA_G0_K, GJKEPA_G1_G, GJKEPA_G1_K, GJKEPA_G2_G, GJKEPA_G2_K, GJKEPA_E0_G, GJKEPA_E0_K, GJKEPA_E0_VCAP,
                   GJKEPA_E0_FCAP, GJKEPA_E1_G, GJKEPA_E1_K, GJKEPA_E1_VCAP, GJKEPA_E1_FCAP, GJKEPA_E2_G, GJKEPA_E2_K,
@@ -762,7 +748,7 @@ const char* gjkepa_version_string(void) {
                   GJKEPA_E4_G, GJKEPA_E4_K, GJKEPA_E4_VCAP, GJKEPA_E4_FCAP, GJKEPA_E5_G, GJKEPA_E5_K, GJKEPA_E5_VCAP,
                   GJKEPA_E5_FCAP, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C1_G,
                   GJKEPA_C1_K, GJKEPA_G0_MINW, GJKEPA_G1_MINW, GJKEPA_G2_MINW, GJKEPA_E0_MINW, GJKEPA_E1_MINW, GJKEPA_E2_MINW,
-                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_E5_MINW, GJKEPA_C0M_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH, GJKEPA_G2_LH,
+                  GJKEPA_E3_MINW, GJKEPA_E4_MINW, GJKEPA_E5_MINW, GJKEPA_C0_MINW, GJKEPA_C1_MINW, GJKEPA_G0_LH, GJKEPA_G1_LH, GJKEPA_G2_LH,
                   GJKEPA_E0_LH, GJKEPA_E1_LH, GJKEPA_E2_LH, GJKEPA_E3_LH, GJKEPA_E4_LH, GJKEPA_E5_LH, GJKEPA_C0_LH,
                   GJKEPA_C1_LH, GJKEPA_SRC_HASH);
     return buf;
@@ -1154,14 +1140,13 @@ int service_ensure(Service* sv, bool check_done, int slot) {
 
 // GJKEPA_QUERY_STATS=1: calls served, mean round trip and mean device time per call, printed at exit
 struct ServiceStats {
-    std::atomic<int64_t> calls{0}, ns{0}, dev_ticks{0}, tick_khz{0}, declined{0};
+    std::atomic<int64_t> calls{0}, ns{0}, dev_ticks{0}, tick_khz{0};
     bool on = std::getenv("GJKEPA_QUERY_STATS") != nullptr;
     ~ServiceStats() {
         if (on && calls > 0 && tick_khz > 0)
-            std::fprintf(stderr, "gjkepa_query service: %lld calls, %.2f us/call round trip, %.2f us/call on the device, "
-                                 "%lld declined\n",
+            std::fprintf(stderr, "gjkepa_query service: %lld calls, %.2f us/call round trip, %.2f us/call on the device\n",
                          (long long)calls.load(), 1e-3 * (double)ns / (double)calls,
-                         1e3 * (double)dev_ticks / (double)tick_khz / (double)calls, (long long)declined.load());
+                         1e3 * (double)dev_ticks / (double)tick_khz / (double)calls);
     }
 } g_sstats;
 
@@ -1252,7 +1237,7 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
     if (n1 < 0 || n2 < 0) return fail(GJKEPA_E_ARG, "negative vertex count");
     int rc = 0;
     Query me{version, tol_ff, p1, p2, n1, n2, {}};
-    Service* sv = service_enabled() && n1 >= 1 && n2 >= 1 && n1 <= GJKEPA_SVC_MAX_HULL && n2 <= GJKEPA_SVC_MAX_HULL &&
+    Service* sv = service_enabled() && n1 >= 1 && n2 >= 1 && n1 <= GJKEPA_MAX_HULL_VERTS && n2 <= GJKEPA_MAX_HULL_VERTS &&
                   device >= 0 && device < device_count_cached() ? service(device) : nullptr;
     const int slot = sv ? service_claim(sv) : -1;
     bool served = false;
@@ -1266,10 +1251,7 @@ int gjkepa_query(int32_t version, double tol_ff, const double* p1, int32_t n1, c
         else
             sv->stuck.fetch_or(1ull << slot, std::memory_order_release);
         if (rc != 0 && rc != kSvcOff) return rc;
-        // a pair the service's lean path declined (its polytope outgrew the small one) is recomputed on
-        // the combining path, which runs the full one-wave path
-        served = rc == 0 && me.rec.status != GJKEPA_SVC_DECLINED;
-        if (g_sstats.on && rc == 0 && !served) g_sstats.declined += 1;
+        served = rc == 0;
     }
     if (!served && !device_state(device, &rc)) return rc;
     if (!served) {
@@ -1348,6 +1330,23 @@ int gjkepa_query_service_stop(int32_t device) {
         if (e != hipSuccess) return hip_fail(e, "query service stop");
     }
     return 0;
+}
+
+int gjkepa_query_service_resident(int32_t device) {
+    std::vector<Service*> svs;
+    {
+        std::lock_guard<std::mutex> g(g_svc_mu);
+        for (size_t d = 0; d < g_svc.size(); ++d)
+            if (g_svc[d] && g_svc[d]->ok == 1 && (device < 0 || (size_t)device == d)) svs.push_back(g_svc[d]);
+    }
+    int resident = 0;
+    for (Service* sv : svs) {
+        if (sv->gen.load(std::memory_order_acquire) == 0) continue;      // never launched
+        const hipError_t e = hipEventQuery(sv->ev);                      // recorded after the latest grid
+        if (e == hipErrorNotReady) resident = 1;
+        else if (e != hipSuccess) return hip_fail(e, "query service state");
+    }
+    return resident;
 }
 
 int gjkepa_query_service_set(int32_t enabled) {

@@ -164,16 +164,6 @@
 #ifndef GJKEPA_C0_MINW
 #define GJKEPA_C0_MINW 3        // A/B r5 (2 rounds): C2 162.7 -> 163.6 M/s, C4 / C5 unchanged (LDS allows 10 waves/CU)
 #endif
-// contact tier 0's main pass leaves contact v2's case_04 (SORT_CLOCK and the polygon containment test,
-// about a quarter of C2's hits) to a full pass of the same hull shape (GJKEPA_CONTACT_C04) or to contact
-// tier 1, so it fits GJKEPA_C0M_MINW waves per SIMD; 0: one full tier-0 pass (A/B)
-#ifndef GJKEPA_C0_DEFER04
-#define GJKEPA_C0_DEFER04 0     // A/B r5 (C2, 2 rounds): one full pass 158.5 / 158.7, deferred 151.9 / 151.9 M/s (3 waves/SIMD, 158 VGPRs)
-#endif
-#ifndef GJKEPA_C0M_MINW
-#define GJKEPA_C0M_MINW (GJKEPA_C0_DEFER04 ? 3 : GJKEPA_C0_MINW)
-#endif
-#define GJKEPA_CONTACT_C04 2    // gjkepa_launch_contact: the tier-0-shaped full pass over route code CT(p) + 1
 #ifndef GJKEPA_C1_G
 #define GJKEPA_C1_G 64
 #endif
@@ -194,9 +184,6 @@
 #endif
 #ifndef GJKEPA_E1_PRIO
 #define GJKEPA_E1_PRIO 2            // wave priority (s_setprio) of EPA tier 1's waves (0: default; A/B r5: C2 +0.2%, C5 +0.6%)
-#endif
-#ifndef GJKEPA_ARGMIN_SHFL
-#define GJKEPA_ARGMIN_SHFL 0        // EPA MINLOC face broadcast by ds_bpermute in groups below 32 lanes (0: LDS slot, A/B)
 #endif
 #ifndef GJKEPA_HORIZON_W16
 #define GJKEPA_HORIZON_W16 1        // horizon twin test on 16-bit edge windows (0: byte compares; A/B r5: C2 +0.6%, C4 +1.6%, C5 +2.2%)
@@ -400,20 +387,11 @@ hipError_t gjkepa_launch_ws_reset(uint32_t* ws, int n32, hipStream_t s);
 #ifndef GJKEPA_SVC_SLOTS
 #define GJKEPA_SVC_SLOTS 64
 #endif
-// The service's waves run a lean one-wave path: hulls of up to GJKEPA_SVC_MAX_HULL vertices (two hull
-// vertices per lane) and EPA's small first polytope only, so a resident wave reserves ~half the
-// registers and a third of the LDS of the full path (what it costs a concurrent batch).  A pair whose
-// polytope outgrows the small one is declined (record status GJKEPA_SVC_DECLINED) and recomputed by
-// the caller on the combining path; larger hulls go there directly.  Records never differ.
-#ifndef GJKEPA_SVC_LEAN
-#define GJKEPA_SVC_LEAN 0        // 1: the lean path (A/B r5: lone call 46.7 vs 44.4 us, the declined pairs' combining round trips; no gain for a concurrent batch)
-#endif
-#ifndef GJKEPA_SVC_MAX_HULL
-#define GJKEPA_SVC_MAX_HULL (GJKEPA_SVC_LEAN ? 128 : GJKEPA_MAX_HULL_VERTS)
-#endif
-#define GJKEPA_SVC_DECLINED 0x7E
+// The service's waves run the full one-wave path (hulls up to GJKEPA_MAX_HULL_VERTS, polytope restarts);
+// a lean variant (hulls <= 128, small polytope only, declining the rest) cost a lone call 2.3 us and a
+// concurrent batch nothing less (A/B r5) and was removed in round 6.
 #ifndef GJKEPA_SVC_MINW
-#define GJKEPA_SVC_MINW (GJKEPA_SVC_LEAN ? 3 : 1)   // lean: 168 VGPRs (21 spilled) instead of 196 (full path: 249)
+#define GJKEPA_SVC_MINW 1
 #endif
 struct alignas(128) gjkepa_svc_slot {
     uint32_t req, stop;              // posted request's sequence number; nonzero: the serving wave exits

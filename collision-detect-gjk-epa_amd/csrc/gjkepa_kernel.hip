@@ -44,18 +44,21 @@ namespace gk {
 constexpr int ST_DEFER = 100;   // internal: does not fit this tier
 constexpr int ST_REDO = 103;    // internal (fp32 compute): answer not certified, recompute in fp64
 constexpr int ST_PARKED = 104;  // internal: polytope parked for the next tier (gjkepa_kernel.h "Polytope parking")
-constexpr int ST_CASE04 = 105;  // internal: contact v2 case_04, left to the full contact pass (contact_kernel DEFER04)
 
 // A compiler-only memory fence (no instruction): LDS reads after it are not hoisted above it.  Without
 // it the scheduler issues a whole hull's K vertex loads (3K VGPRs in fp64: 6 per vertex) ahead of the
 // dot products, and for hull B while hull A's are still live, which is where most of the GJK / EPA
 // tiers' register peaks and scratch spills came from.
 DEV void gk_lds_fence() { asm volatile("" ::: "memory"); }
-#ifndef GJKEPA_SCREEN_FENCE
-#define GJKEPA_SCREEN_FENCE 0    // fence between hull A's and hull B's fp32-screened support scans
+// Per group width: the small-hull tiers (G < 32) lose by a fence (the hoisted loads are their memory-level
+// parallelism: C2 -3 to -4% in round 5), the wide large-hull tiers spill without one.  A/B r6 (2 rounds):
+// GJK tier 2's screen fenced (65 -> 14 spilled VGPRs) C4 42.55 -> 42.90; with EPA tier 3's dots too (52 -> 0)
+// 42.98; the dots fence in GJK tier 1 or the 64-lane contact tier costs C5 0.7% / 0.3%, so it is EPA only.
+#ifndef GJKEPA_SCREEN_FENCE_MIN_G
+#define GJKEPA_SCREEN_FENCE_MIN_G 32  // fence between hull A's and hull B's fp32-screened scans in tiers with G >= this (0: none)
 #endif
-#ifndef GJKEPA_DOTS_FENCE_MIN_K
-#define GJKEPA_DOTS_FENCE_MIN_K 0   // support_dots: fence between the two hulls' reads in tiers with K >= this (0: none)
+#ifndef GJKEPA_DOTS_FENCE_MIN_G
+#define GJKEPA_DOTS_FENCE_MIN_G 64    // support_dots: fence between the two hulls' reads in EPA tiers with G >= this and K >= 4 (0: none)
 #endif
 
 // fp32 certificate.  An fp32 EPA can build an invalid polytope from inconsistent visibility decisions
@@ -63,10 +66,11 @@ DEV void gk_lds_fence() { asm volatile("" ::: "memory"); }
 // drops and it may stop far from the penetration depth (C5: 20% low, normal off by 0.4 rad on one
 // pair in 2^20).  In exact arithmetic EPA's MINLOC distance never decreases (each polytope contains
 // the last) and at termination the support along the final normal lies on the final face, so the
-// fp32 path checks both: a drop of more than CERT_DROP * max(1, d) between iterations, or a support
-// gap h_M(n) - d above CERT_GAP * max(1, d) when EPA stops, sends the pair to the redo launch, which
-// recomputes it whole in fp64 (so do fp32 error statuses that fp64 may not share).  A certified
-// answer has d <= h_M(n) <= d + gap, and d cannot exceed the depth of the polytope it came from.
+// fp32 path checks both: a drop of more than CERT_DROP * d between iterations, or a support gap
+// h_M(n) - d plus its fp32 evaluation noise (CERT_NOISE * (|A| + |B|)) above CERT_GAP * d when EPA stops,
+// sends the pair to the redo launch, which recomputes it whole in fp64 (so do fp32 error statuses that
+// fp64 may not share, and a polytope the origin is not strictly inside).  A certified answer has
+// d <= h_M(n) <= d + gap, and d cannot exceed the depth of the polytope it came from.
 template <typename T> DEV constexpr bool certify() { return sizeof(T) == 4; }
 // fp32 compute: an EPA / contact outcome the fp64 recomputation may answer differently
 template <typename T> DEV bool redo_status(int r, bool last_tier) {
@@ -346,7 +350,7 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
     T (&ta)[K] = D.t[0];
     T (&tb)[K] = D.t[1];
     T va = -Tol<T>::BIG, vb = -Tol<T>::BIG;
-    if constexpr (GJKEPA_DOTS_FENCE_MIN_K > 0 && K >= GJKEPA_DOTS_FENCE_MIN_K) {
+    if constexpr (GJKEPA_DOTS_FENCE_MIN_G > 0 && G >= GJKEPA_DOTS_FENCE_MIN_G && K >= 4 && VC > 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
@@ -393,9 +397,8 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
 CTX_T DEV void support_idx(const CTX& c, V3<T> d, int& ia, int& ib) {
     if constexpr (ScreenOn<K>::value && sizeof(T) == 8 && sizeof(TH) == 4) {
         screened_idx(c, d, 0, c.vmax_a, ia);
-#if GJKEPA_SCREEN_FENCE
-        gk_lds_fence();                  // hull B's screen reads its vertices after hull A's is done
-#endif
+        if constexpr (GJKEPA_SCREEN_FENCE_MIN_G > 0 && G >= GJKEPA_SCREEN_FENCE_MIN_G)
+            gk_lds_fence();              // hull B's screen reads its vertices after hull A's is done
         screened_idx(c, d, 1, c.vmax_b, ib);
         return;
     }
@@ -815,23 +818,6 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& ne
         const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
         m = c.g.ballot(tie && kk == kmin);
     }
-    if constexpr (GJKEPA_ARGMIN_SHFL && G < 32) {
-        // the winner's row, selected on every lane, then pulled from the winner lane with ds_bpermute:
-        // no LDS slot write / read round trip (groups of 32 and 64 lanes keep the slot: a v_readlane
-        // broadcast lost there, round 3)
-        T bx = 0, by = 0, bz = 0;
-        uint32_t bw = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (rr == r) { bx = F.nx[r]; by = F.ny[r]; bz = F.nz[r]; bw = (F.fv[r] & 0xffu) | (F.d[r] < T(0) ? 0x80000000u : 0u); }
-        const int src = m ? (int)__builtin_ctzll(m) : c.g.lane;     // m: absolute lane bits of this group
-        dmin = vmin;
-        n = vmk<T>(__shfl(bx, src), __shfl(by, src), __shfl(bz, src));
-        const uint32_t bv = (uint32_t)__shfl((int)bw, src);
-        neg = (bv >> 31) != 0;
-        av = (int)(bv & 0xffu);
-        return;
-    }
     if (c.g.bit(m)) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -1099,7 +1085,7 @@ CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     const T prev = S.minv;
     face_argmin(c, S.F, S.minv, S.dir, S.neg, S.av);
     if constexpr (certify<T>()) {                             // fp32 certificate: MINLOC never drops
-        if (c.g.unib(S.minv < prev - Tol<T>::CERT_DROP * (prev > T(1) ? prev : T(1)))) return ST_REDO;
+        if (c.g.unib(S.minv < prev - Tol<T>::CERT_DROP * prev)) return ST_REDO;
     }
     // dot(a1 - O, n) is -DIST_PF_SIGN(O, face) (exact negation; a zero's sign never matters here):
     // negative iff the face's signed distance is positive
@@ -1110,17 +1096,16 @@ CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
     else stop = S.F1 > F2;
     GK_STAMP(SE_TERM);
     if constexpr (certify<T>()) {
-        // fp32 certificate at termination: closed support gap; a depth above fp32 resolution; the
-        // origin strictly below every face (a hit the polytope itself proves)
+        // fp32 certificate at termination: support gap plus its evaluation noise within CERT_GAP x d (a
+        // touching pair, d below the noise, never passes); the origin strictly below every face (a hit
+        // the polytope itself proves)
         if (stop) {
             constexpr int R = (FC + G - 1) / G;
             bool out = false;
 #pragma unroll
             for (int r = 0; r < R; ++r) out = out || (!(S.F.fv[r] & kEmpty) && !(S.F.d[r] < T(0)));
             const float sc = c.vmax_a + c.vmax_b;
-            if (c.g.any(out) ||
-                c.g.unib(S.hsup - S.minv > Tol<T>::CERT_GAP * (S.minv > T(1) ? S.minv : T(1)) ||
-                         !(S.minv > Tol<T>::CERT_TOUCH * (sc > 1.0f ? sc : 1.0f))))
+            if (c.g.any(out) || c.g.unib(!(S.hsup - S.minv + Tol<T>::CERT_NOISE * sc <= Tol<T>::CERT_GAP * S.minv)))
                 return ST_REDO;
         }
     }
@@ -1665,12 +1650,8 @@ CTX_T DEV int contact_case04_lds(CTX& c, int na, V3<T> b0, V3<T> b1, V3<T>& res)
 #define GJKEPA_CASE04_LDS 1      // case_04 reads its point sets from LDS (0: register copies, A/B)
 #endif
 
-// get_collisionPoint_02 (:457-696).  DEFER04: case_04 (SORT_CLOCK + polygon containment, a quarter of
-// C2's hits) is not computed here: ST_CASE04 hands the pair to the full contact pass, so the common
-// kernel does not carry case_04's registers (contact_kernel).
-template <bool DEFER04 = false, typename T, typename TH, int G, int K, int VC, int FC, int LH>
-DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
-    auto& C = c.L.u.c;
+// get_collisionPoint_02 (:457-696)
+CTX_T DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
     const T band = T(0.1);
     const T t1 = D.m[0] - band, t2 = D.m[1] - band;                 // :471-472
     const int n1 = band_set(c, 0, D, t1, false);
@@ -1696,8 +1677,6 @@ DEV int contact_v2(CTX& c, const DotSet<T, K>& D, V3<T>& res) {
         V3<T> f1, f2;
         foot_ll(a0, a1, set_pt(c, 0), set_pt(c, 1), f1, f2);
         res = vdiv(vadd(f1, f2), T(2));
-    } else if (DEFER04 && ((n1 == 2 && n2 >= 3) || (n1 >= 3 && n2 == 2))) {
-        return ST_CASE04;
     } else if (n1 == 2 && n2 >= 3) {                               // case_04(SPT_p2, SPT_p1)
         band_set(c, 0, D, t1, true);
         const V3<T> q0 = set_pt(c, 0), q1 = set_pt(c, 1);
@@ -2013,8 +1992,7 @@ CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t
 
 // EPA_solu's post-processing (:326-343) for EPA depth and normal n: nearest points, contact point
 // (version_ 1/2/3) and contact type.  Returns -type (o13 filled) or an error status.
-template <bool DEFER04 = false, typename T, typename TH, int G, int K, int VC, int FC, int LH>
-DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
+CTX_T DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
     int st;
     int ia, ib;
     GK_STAMP(SE_TERM);
@@ -2028,7 +2006,7 @@ DEV int contact_phase(CTX& c, T depth, V3<T> n, int version, T tol_ff, T* o13) {
     // contact point, so the dots are dead during case_04 (the contact kernel's register peak)
     int type = (version == 1 || version == 2) ? collision_type(c, D, tol_ff) : 0;
     if (version == 1) st = contact_v1(c, n, D, pt);                       // :329-340
-    else if (version == 2) st = contact_v2<DEFER04>(c, D, pt);
+    else if (version == 2) st = contact_v2(c, D, pt);
     else if (version == 3) { V3<T> nw; st = contact_v3(c, n, pt, nw); n = nw; }
     else st = GJKEPA_STATUS_BAD_VERSION;
     GK_STAMP(SE_CONT);
@@ -2644,9 +2622,7 @@ template <typename TIn, typename T, int K> using QLds = Lds<T, TIn, 64, K, GJKEP
 template <typename TIn, typename T, int K> using QLdsS = Lds<T, TIn, 64, K, GJKEPA_Q_VCAP, GJKEPA_Q_FCAP, true>;
 // RT: the record's field type (T, or float for the fp32 chain's fp64 redo).  Returns true when an fp32
 // answer is not certified (certify<T>(): nothing stored; the caller recomputes the pair in fp64).
-// LEAN (the resident service): no restart with the last tier's polytope; an overflowing pair is stored
-// with status GJKEPA_SVC_DECLINED for the caller to recompute on the full path.
-template <typename TIn, typename T, int K, typename RT = T, bool LEAN = false>
+template <typename TIn, typename T, int K, typename RT = T>
 DEV bool query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, const TIn* pb, int na, int nb,
                       int version, T tol_ff, void* out, int64_t pair) {
     using LB = QLds<TIn, T, K>;
@@ -2683,12 +2659,7 @@ DEV bool query_pair_k(unsigned char* smem, const Grp<64>& grp, const TIn* pa, co
     uint32_t de = 0;
     r = epa_phase(c, kc, depth, n, de);
     __builtin_amdgcn_wave_barrier();
-    if constexpr (LEAN) {
-        if (r == ST_DEFER) {                             // declined: the caller runs the full path
-            store_record<64, RT>(out, pair, gl, o, 0, 0, GJKEPA_SVC_DECLINED, 0u);
-            return false;
-        }
-    } else if (r == ST_DEFER) {                          // small polytope full: the last tier's from the simplex
+    if (r == ST_DEFER) {                                 // small polytope full: the last tier's from the simplex
         Ctx<T, TIn, 64, K, GJKEPA_E5_VCAP, GJKEPA_E5_FCAP, 2> cb{*reinterpret_cast<QLds<TIn, T, K>*>(smem), grp};
         cb.na = na;
         cb.nb = nb;
@@ -2814,20 +2785,7 @@ __global__ __launch_bounds__(64, GJKEPA_SVC_MINW) void service_kernel(const gjke
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h, 7) << 32);
             const double tol = __builtin_bit_cast(double, tb);
             const int ca = na < 0 || na > GJKEPA_MAX_HULL_VERTS ? 0 : na;
-            const int nmax = na > nb ? na : nb;
-            if (!GJKEPA_SVC_LEAN) {
-                query_pair<double, double>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
-            } else if (na < 1 || nb < 1 || nmax > GJKEPA_SVC_MAX_HULL) {   // bad sizes / large hulls: declined
-                double o[13];
-#pragma unroll
-                for (int i = 0; i < 13; ++i) o[i] = 0.0;
-                store_record<64, double>(sl->rec, 0, grp.gl, o, 0, 0, GJKEPA_SVC_DECLINED, 0u);
-            } else if (nmax <= 64) {
-                query_pair_k<double, double, 1, double, true>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
-            } else {
-                static_assert(!GJKEPA_SVC_LEAN || GJKEPA_SVC_MAX_HULL <= 128, "the service's hull depth is two vertices per lane");
-                query_pair_k<double, double, 2, double, true>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
-            }
+            query_pair<double, double>(smem, grp, sl->v, sl->v + 3 * ca, na, nb, version, tol, sl->rec, 0);
             __builtin_amdgcn_wave_barrier();
             GK_STAMP_END();
             const uint64_t t_done = wall_clock64();
@@ -2865,11 +2823,8 @@ __global__ __launch_bounds__(64, GJKEPA_SVC_MINW) void service_kernel(const gjke
 #endif  // GK_IN(0)
 
 // Contact kernel: nearest points, contact point and contact type (:326-343) for every pair EPA
-// finished, from the depth and normal it parked; writes the final record.  DEFER04 (contact tier 0's
-// main pass): a version-2 pair that takes case_04 goes on to route code route_code + 1 unanswered — the
-// full pass of the same fork point (contact tier 1, or the tier-0-shaped case_04 pass) — so this kernel
-// fits three waves per SIMD (158 VGPRs instead of 256).
-template <typename TIn, typename T, int G, int K, int MINW, bool LH, bool DEFER04>
+// finished, from the depth and normal it parked; writes the final record.
+template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args a) {
     using L_t = Lds<T, TIn, G, K, 0, 1>;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -2899,13 +2854,11 @@ __global__ __launch_bounds__(64, MINW) void contact_kernel(const gjkepa_epa_args
 #pragma unroll
         for (int i = 0; i < 13; ++i) o13[i] = T(0);
 #else
-        const int r = contact_phase<DEFER04>(c, depth, n, a.version, (T)a.tol_ff, o13);
+        const int r = contact_phase(c, depth, n, a.version, (T)a.tol_ff, o13);
 #endif
         __builtin_amdgcn_wave_barrier();
         uint8_t next = 0;
-        if (DEFER04 && r == ST_CASE04) {
-            next = (uint8_t)(a.route_code + 1);
-        } else if (r < 0) {
+        if (r < 0) {
             store_record<G, T>(a.out, pair, gl, o13, 1, -r, 0, diag);
         } else if (redo_status<T>(r, false)) {   // fp32: contact-phase error, recomputed in fp64
             next = GJKEPA_ROUTE_REDO;
@@ -3013,9 +2966,9 @@ hipError_t launch_epa(const gjkepa_epa_args& a, hipStream_t s) {
                     (GJKEPA_E##t##_LH != 0)
 
 #if GK_IN(3)
-template <typename TIn, typename T, int G, int K, int MINW, bool LH, bool DEFER04>
+template <typename TIn, typename T, int G, int K, int MINW, bool LH>
 hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
-    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH, DEFER04>;
+    auto kfn = gk::contact_kernel<TIn, T, G, K, MINW, LH>;
     constexpr int GPW = 64 / G;
     const size_t lds = gk::lds_stride<gk::Lds<T, TIn, G, K, 0, 1>, G>() * GPW;
     int grid;
@@ -3027,15 +2980,12 @@ hipError_t launch_contact(const gjkepa_epa_args& a, hipStream_t s) {
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
-// tier 0: the main small-hull pass (case_04 deferred to route code + 1); 1: large hulls (full);
-// GJKEPA_CONTACT_C04: the small-hull full pass for the deferred case_04 pairs
+// tier 0: small hulls; 1: large hulls
 template <typename TIn, typename T>
 hipError_t contact_any(int tier, const gjkepa_epa_args& a, hipStream_t s) {
     if (tier == 0)
-        return launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0M_MINW, (GJKEPA_C0_LH != 0), (GJKEPA_C0_DEFER04 != 0)>(a, s);
-    if (tier == GJKEPA_CONTACT_C04)
-        return launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0), false>(a, s);
-    return launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0), false>(a, s);
+        return launch_contact<TIn, T, GJKEPA_C0_G, GJKEPA_C0_K, GJKEPA_C0_MINW, (GJKEPA_C0_LH != 0)>(a, s);
+    return launch_contact<TIn, T, GJKEPA_C1_G, GJKEPA_C1_K, GJKEPA_C1_MINW, (GJKEPA_C1_LH != 0)>(a, s);
 }
 #endif
 
@@ -3102,8 +3052,7 @@ extern "C" int gjkepa_diag_stamps(unsigned long long* out, int reset) {
 #endif
 
 hipError_t gjkepa_launch_service(const gjkepa_svc_args& a, int n_slots, hipStream_t s) {
-    // the lean path's image (small polytope, K <= 2), or the full path's
-    using L_t = std::conditional_t<GJKEPA_SVC_LEAN != 0, gk::QLdsS<double, double, 2>, gk::QLds<double, double, GJKEPA_MAX_HULL_VERTS / 64>>;
+    using L_t = gk::QLds<double, double, GJKEPA_MAX_HULL_VERTS / 64>;
     hipLaunchKernelGGL(gk::service_kernel, dim3((unsigned)n_slots), dim3(64), sizeof(L_t), s, a);
     return hipGetLastError();
 }

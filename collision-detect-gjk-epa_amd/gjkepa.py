@@ -35,13 +35,14 @@ EXPORTS = (
     "gjkepa_compact_workspace_bytes", "gjkepa_compact_hits_device", "gjkepa_batch_warm_device",
     "gjkepa_collide", "gjkepa_shard_range", "gjkepa_batch_multi", "gjkepa_comm_unique_id", "gjkepa_comm_init",
     "gjkepa_comm_destroy", "gjkepa_comm_backend", "gjkepa_allgather_records_device",
-    "gjkepa_query_service_stop", "gjkepa_query_service_set", "gjkepa_workspace_bytes_for",
+    "gjkepa_query_service_stop", "gjkepa_query_service_set", "gjkepa_query_service_resident", "gjkepa_workspace_bytes_for",
     "gjkepa_launch_timing", "gjkepa_launch_timing_read",
 )
 COMM_ID_BYTES = 128
 # workspace header word counting the park slots a gjkepa_batch_device call took (diagnostics; csrc/
 # gjkepa_capi.cpp kWsParkWord = GJKEPA_WS_COUNTERS + GJKEPA_WS_TALLY)
-WS_PARK_WORD = 40 + 48
+WS_COUNTERS, WS_TALLY = 40, 48   # gjkepa_kernel.h GJKEPA_WS_COUNTERS / GJKEPA_WS_TALLY (uint32 words)
+WS_PARK_WORD = WS_COUNTERS + WS_TALLY
 HULL_MAX_POINTS = 256
 
 REC64 = np.dtype([
@@ -145,6 +146,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.gjkepa_query_service_stop.restype = ctypes.c_int
     lib.gjkepa_query_service_set.argtypes = [c_i32]
     lib.gjkepa_query_service_set.restype = ctypes.c_int
+    lib.gjkepa_query_service_resident.argtypes = [c_i32]
+    lib.gjkepa_query_service_resident.restype = ctypes.c_int
     lib.gjkepa_workspace_bytes_for.argtypes = [c_i64, c_i64]
     lib.gjkepa_workspace_bytes_for.restype = c_i64
     lib.gjkepa_launch_timing.argtypes = [c_i32]
@@ -200,6 +203,13 @@ def query_service_stop(device: int = -1) -> None:
     """Drain the resident grid behind gjkepa() (include/gjkepa.h): call before a device-wide
     synchronisation such as torch.cuda.synchronize() while single-pair calls may have run."""
     _check(load().gjkepa_query_service_stop(int(device)), "gjkepa_query_service_stop")
+
+
+def query_service_resident(device: int = -1) -> bool:
+    """Whether a resident service grid is still on the GPU (gjkepa_query_service_resident)."""
+    rc = load().gjkepa_query_service_resident(int(device))
+    _check(min(rc, 0), "gjkepa_query_service_resident")
+    return rc == 1
 
 
 def query_service_set(enabled: bool) -> bool:

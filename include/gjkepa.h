@@ -134,6 +134,9 @@ int gjkepa_query_service_stop(int32_t device);
  * The initial setting is on unless the environment sets GJKEPA_QUERY_SERVICE=0.  Returns the
  * previous setting (0/1) or a negative GJKEPA_E_* code. */
 int gjkepa_query_service_set(int32_t enabled);
+/* Diagnostic: 1 while a service grid of `device` (device < 0: any device) is still on the GPU, 0 when
+ * none is, or a negative GJKEPA_E_* code.  Non-blocking. */
+int gjkepa_query_service_resident(int32_t device);
 
 /* ---- batch over host buffers (blocking) ------------------------------------------------------
  * verts:     hull vertex pool, dtype `vert_dtype`, n_vert_scalars scalars in total.

@@ -349,10 +349,11 @@ static int cmp_dbl(const void* a, const void* b) {
 /* diagnostic: nonzero -> epa() prints one line per iteration to stderr (single-threaded use only) */
 int oracle_epa_trace = 0;
 /* fp32 certificate thresholds (ORC_F32 only; see gjkepa_kernel.hip "fp32 certificate"): the largest
- * drop of the polytope's MINLOC distance between iterations, and the largest support gap
- * h_M(n) - depth at termination, both relative to max(1, depth). */
-double oracle_cert_drop = 5e-7, oracle_cert_gap = 5e-7, oracle_cert_touch = 1e-5;
-static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: touch / outside */
+ * drop of the polytope's MINLOC distance between iterations, relative to that distance, and the largest
+ * support gap h_M(n) - depth at termination plus the fp32 evaluation noise of both terms
+ * (oracle_cert_noise x (|A| + |B|), |A| the largest |coordinate| of hull A), relative to the depth. */
+double oracle_cert_drop = 5e-7, oracle_cert_gap = 5e-7, oracle_cert_noise = 2.384185791015625e-07;   /* 4 x 2^-24 */
+static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: origin not inside */
 static _Thread_local double g_cert_scale;   /* max |coordinate| of A + that of B */
 #include <stdio.h>
 
@@ -455,14 +456,12 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
                     iter, F1, F2, (double)minv, (double)dir.x, (double)dir.y, (double)dir.z, (double)sp.x,
                     (double)sp.y, (double)sp.z, (double)dot(sp, dir), (double)minv2, stop);
         {
-            double sc = minv > 1.0 ? minv : 1.0;
-            if (minv2 < minv - oracle_cert_drop * sc) g_cert |= 1;
-            if (stop && dot(sp, dir) - minv2 > oracle_cert_gap * sc) g_cert |= 2;
+            if (minv2 < minv - oracle_cert_drop * minv) g_cert |= 1;
+            if (stop && !(dot(sp, dir) - minv2 + oracle_cert_noise * g_cert_scale <= oracle_cert_gap * minv2)) g_cert |= 2;
             if (stop) {
                 int out = 0;
                 for (int f = 0; f < F2; ++f) out |= !(H->f[f].sd < 0.0);
-                double ts = g_cert_scale > 1.0 ? g_cert_scale : 1.0;
-                if (out || !(minv2 > oracle_cert_touch * ts)) g_cert |= 8;
+                if (out) g_cert |= 8;
             }
         }
         if (stop) { *depth = minv2; *normal = dir2; return 0; }

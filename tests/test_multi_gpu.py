@@ -120,6 +120,53 @@ def test_rccl_comm_world1_allgather():
     assert gjkepa.Comm.backend() != "unavailable"
 
 
+def test_record_exchange_rccl_overlapped_steps():
+    """shard.RecordExchange's RCCL branch, the one bench.py runs at N > 1 over the library's
+    communicator (world 1 here): double-buffered records, each step's all-gather on the exchange's own
+    stream after that step's kernels, the next step's kernels overlapping it.  Four steps of
+    gjkepa_batch_device over four different pair sets alternate between the two buffers; after each
+    step `last_gathered` holds that step's records, and the other buffer still holds the previous
+    step's (the compute stream waited for its gather before reusing it, and nothing wrote it early)."""
+    import torch
+
+    import shard
+
+    dev = torch.device("cuda", 0)
+    comm = gjkepa.Comm(1, 0, gjkepa.Comm.unique_id(), 0)
+    try:
+        n = 1 << 16
+        prec = gjkepa.PREC_F64
+        rb = gjkepa.load().gjkepa_record_bytes(prec)
+        pools = [gjkepa.synth_pairs(SEED + 17 * s, n, 32, 32, 2.5, dtype=np.float32) for s in range(4)]
+        refs = [gjkepa.gjkepa_batch(p, 2, 1.0) for p in pools]
+        assert len({r.tobytes() for r in refs}) == 4
+        dpools = [[torch.from_numpy(a).to(dev) for a in (p.verts, p.hull_off, p.hull_cnt, p.pairs.reshape(-1))]
+                  for p in pools]
+        wsb = gjkepa.workspace_bytes_for(n, max(gjkepa.large_pairs(p) for p in pools))
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+        ex = shard.RecordExchange(n * rb, 1, 0, dev, prec, comm=comm)
+        assert ex.overlap and len(ex.gathered) == 2
+        stream = torch.cuda.current_stream(dev)
+        for i, (v, o, c, p) in enumerate(dpools):
+            buf = ex.buffer(stream)                   # waits for the gather that last read this buffer
+            assert buf.data_ptr() == ex.gathered[i % 2].data_ptr()
+            gjkepa.gjkepa_batch_device(2, 1.0, gjkepa.DTYPE_F32, prec, v.data_ptr(), o.data_ptr(), c.data_ptr(),
+                                       p.data_ptr(), n, buf.data_ptr(), ws.data_ptr(), wsb, stream.cuda_stream)
+            ex.submit(stream)
+            if i >= 1:                                 # the previous step's buffer, while this step's gather may run
+                prev = ex.gathered[(i - 1) % 2].cpu().numpy().tobytes()
+                assert prev == refs[i - 1].tobytes(), i
+            torch.cuda.synchronize(dev)
+            assert ex.last_gathered.cpu().numpy().tobytes() == refs[i].tobytes(), i
+            assert ex.last.cpu().numpy().tobytes() == refs[i].tobytes(), i
+        ex.drain()
+        assert all(e is None for e in ex.done)
+        assert ex.gathered[0].cpu().numpy().tobytes() == refs[2].tobytes()
+        assert ex.gathered[1].cpu().numpy().tobytes() == refs[3].tobytes()
+    finally:
+        comm.close()
+
+
 def test_two_rank_bench_verifies_its_exchange(tmp_path):
     """bench.py at N = 2 (torch.distributed.run, one process per rank, gloo control plane, both ranks
     on this box's one GPU, host-staged record exchange): each rank runs its shard through the library

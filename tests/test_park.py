@@ -68,10 +68,11 @@ def test_parked_fp32_chain_matches_unparked():
 
 def test_parked_in_overlapped_chain(orc, tmp_path):
     """Parking inside the overlapped chain (batches from 64K pairs: EPA tier 0 in parts, contact passes
-    forked onto internal streams, EPA tiers 2 and 3 side by side): full park area, park slots sized by
-    gjkepa_workspace_bytes_for, none at all, and in a fresh process the other schedules (EPA tier 2 in two
-    parts on two streams with its forked passes claiming single chunks; tiers 2 and 3 in sequence) — all
-    byte-identical to each other and to the oracle."""
+    forked onto internal streams, EPA tiers 2 and 3 in sequence, the default): full park area, park slots
+    sized by gjkepa_workspace_bytes_for, none at all, and in fresh processes the other schedules (EPA tier 2
+    in two parts on two streams with its forked passes claiming single chunks; EPA tiers 2 and 3 side by
+    side on two streams, GJKEPA_E23_STREAMS=2: tier 3 forked after tier 1 and joined before tier 4, tier-2
+    overflow routed straight to tier 4) — all byte-identical to each other and to the oracle."""
     import os
     import subprocess
     import sys
@@ -93,7 +94,7 @@ def test_parked_in_overlapped_chain(orc, tmp_path):
         "z = np.load(sys.argv[2]); p = gjkepa.HullPool(z['verts'], z['off'], z['cnt'], z['pairs'])\n"
         "np.save(sys.argv[3], gjkepa.gjkepa_batch(p, 2, 1.0).view(np.uint8))\n")
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "collision-detect-gjk-epa_amd")
-    for k, env in enumerate([{"GJKEPA_EPA2_PARTS": "2", "GJKEPA_E23_STREAMS": "1"}, {"GJKEPA_E23_STREAMS": "1"}]):
+    for k, env in enumerate([{"GJKEPA_EPA2_PARTS": "2", "GJKEPA_E23_STREAMS": "1"}, {"GJKEPA_E23_STREAMS": "2"}]):
         outp = tmp_path / f"r{k}.npy"
         r = subprocess.run([sys.executable, "-c", script, pkg, str(tmp_path / "pool.npz"), str(outp)],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=100)

@@ -93,11 +93,12 @@ def test_stop_then_device_synchronize_returns_promptly(orc):
     t = time.perf_counter()
     gjkepa.query_service_stop(0)
     t_stop = time.perf_counter() - t
+    assert not gjkepa.query_service_resident(0)   # the grid's completion event, not a wall clock
     t = time.perf_counter()
     torch.cuda.synchronize()
     t_sync = time.perf_counter() - t
     assert t_stop < 0.5, t_stop
-    assert t_sync < 0.0015, f"synchronize after stop took {t_sync * 1e3:.2f} ms (idle drain is 2 ms)"
+    assert t_sync < 0.05, f"synchronize after stop took {t_sync * 1e3:.2f} ms"
     got = [gjkepa.gjkepa(*q) for q in qs]  # relaunched
     _check(orc, qs, got)
     gjkepa.query_service_stop(-1)          # all devices; nothing running is fine too
@@ -186,11 +187,16 @@ def test_service_off_while_calls_in_flight(orc):
         stop_evt.set()
         for x in th:
             x.join()
+    # no grid left on the GPU (checked on the grid's own completion event), so a device-wide
+    # synchronisation does not wait for one; its time is bounded loosely (a resident grid would hold it
+    # for GJKEPA_SVC_IDLE_US = 2 ms at least)
+    resident = gjkepa.query_service_resident(0)
     t = time.perf_counter()
     torch.cuda.synchronize()
     t_sync = time.perf_counter() - t
     try:
-        assert t_sync < 0.0015, f"synchronize with the service off took {t_sync * 1e3:.2f} ms"
+        assert not resident, "a service grid is still resident after gjkepa_query_service_set(0)"
+        assert t_sync < 0.05, f"synchronize with the service off took {t_sync * 1e3:.2f} ms"
         got = [c for o in outs for _, c in o]
         idx = [k for o in outs for k, _ in o]
         assert len(got) > 50

@@ -6,7 +6,7 @@ fp32 build of the oracle, with the pairs its certificate flags replaced by the f
 sweeps the model's certificate thresholds (oracle_cert_drop / oracle_cert_gap: the float globals of
 libgjkepa_oracle_f32.so, the same values as csrc/gk_common.h Tol<float>::CERT_*) and reports, per
 config and threshold, the pairs sent to the fp64 redo and the gate metrics of tools/fp32_metrics.py at
-a normal bound of 1e-3 rad.  usage: python tools/fp32_cert_sweep.py [C2 C5 C4] [--pairs N]
+the gate's normal bound.  Swept: the noise allowance, k x 2^-24 x (|A| + |B|), added to the support gap.  usage: python tools/fp32_cert_sweep.py [C2 C5 C4] [--pairs N]
 """
 from __future__ import annotations
 
@@ -28,12 +28,13 @@ from fp32_check import model_fp32  # noqa: E402
 from fp32_metrics import fp32_report  # noqa: E402
 
 
-def set_cert(gap: float, drop: float) -> None:
+def set_cert(gap: float, drop: float, noise: float) -> None:
     oracle.gjkepa_batch_f32(gjkepa.HullPool(np.zeros(0, np.float32), np.zeros(0, np.int64), np.zeros(0, np.int32),
                                             np.zeros((0, 2), np.int32)))          # loads the f32 library
     lib = oracle._lib32
     ctypes.c_float.in_dll(lib, "oracle_cert_gap").value = gap
     ctypes.c_float.in_dll(lib, "oracle_cert_drop").value = drop
+    ctypes.c_float.in_dll(lib, "oracle_cert_noise").value = noise
 
 
 def main():
@@ -45,12 +46,13 @@ def main():
         n = npairs or n
         pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax, dtype=np.float32)
         r64 = oracle.gjkepa_batch(pool, 2, 1.0, threads)
-        for thr in (1e-5, 1e-6, 5e-7, 2.5e-7):
-            set_cert(thr, thr)
+        for thr, k in ((5e-7, 0), (5e-7, 2), (5e-7, 4), (5e-7, 8)):
+            set_cert(thr, thr, k * 2.0 ** -24)
             m, redo = model_fp32(pool, r64, threads)
-            rep = fp32_report(pool, m, r64, angle=1e-3)
+            rep = fp32_report(pool, m, r64)
             rep.pop("gate", None)
-            print(json.dumps({"config": cfg, "pairs": n, "cert": thr, "redo": int(redo.sum()), **rep}), flush=True)
+            print(json.dumps({"config": cfg, "pairs": n, "cert": thr, "noise_ulps": k, "redo": int(redo.sum()),
+                              "redo_frac": round(float(redo.mean()), 4), **rep}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Print the headline fields of a bench line (or, with --ab DIR, the A/B lines of tools/gpu_r5.sh)."""
+"""Print the headline fields of a bench line (or, with --ab DIR, the A/B lines of tools/gpu_session.sh step ab)."""
 import glob
 import json
 import os

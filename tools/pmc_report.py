@@ -10,7 +10,8 @@ issue slot (32 lanes/clock) against 1024 SIMDs x the chain's kernel time x 2.4 G
 longer, so this is a lower bound on VALU-pipe occupancy).
 The entry carries the library source hash the passes ran (gjkepa_version_string); bench.py uses
 it only when the loaded library has the same hash.
-usage: python tools/pmc_report.py <gpurun_out tag> <key> <n_pairs>  (merges into profiles/pmc_traffic.json)"""
+usage: python tools/pmc_report.py <dir> <key> <n_pairs>  (merges into profiles/pmc_traffic.json); <dir> holds
+the passes p1..p5 (tools/gpu_session.sh step pmc: gpurun_out/<tag>/pmc_<config>)"""
 import collections
 import csv
 import glob
@@ -23,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     tag, key, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    base = os.path.join(ROOT, "gpurun_out", tag, "pmc")
+    base = tag if os.path.isdir(tag) else os.path.join(ROOT, "gpurun_out", tag, "pmc")
     per = collections.defaultdict(lambda: collections.defaultdict(dict))
     dur = collections.defaultdict(dict)
     for f in sorted(glob.glob(f"{base}/p*/run_counter_collection.csv")):
