@@ -194,6 +194,13 @@
 #ifndef GJKEPA_EPA_HPACK
 #define GJKEPA_EPA_HPACK 1          // one-word horizon edges, FC / 2 of them, where keys fit 16 bits (0: A/B r5 C2 157.3 -> 162.7)
 #endif
+#ifndef GJKEPA_PAD_V0
+#define GJKEPA_PAD_V0 1             // hull slots past the count hold vertex 0 again; support scans skip the mask
+                                    // (A/B r6, 3 rounds: C2 +1.1%, C4 +1.6%, C5 +1.9%; 0: masked)
+#endif
+#ifndef GJKEPA_DOTS_FMAX
+#define GJKEPA_DOTS_FMAX 1          // support_dots' per-lane maximum on v_max_f64 (0: compare + selects, A/B)
+#endif
 #ifndef GJKEPA_EPA_PLACE
 #define GJKEPA_EPA_PLACE 1          // EPA new faces built on the lane that owns their slot (0: staged in LDS, A/B)
 #endif

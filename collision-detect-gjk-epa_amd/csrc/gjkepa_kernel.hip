@@ -299,9 +299,11 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
-        const V3<TH> v = c.raw(h, i < n ? i : 0);
+        // GJKEPA_PAD_V0: slots past the count hold vertex 0 again, whose screen value can only make
+        // vertex 0's duplicates candidates too (then the full path below takes the lowest index)
+        const V3<TH> v = c.raw(h, GJKEPA_PAD_V0 || i < n ? i : 0);
         const float t = sg * fmaf(fz, v.z, fmaf(fy, v.y, fx * v.x));
-        sv[k] = i < n ? t : -FLT_MAX;
+        sv[k] = GJKEPA_PAD_V0 || i < n ? t : -FLT_MAX;
         m = fmaxf(m, sv[k]);
     }
     m = gmax<G>(m);
@@ -313,7 +315,7 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
-        if (i < n && !(sv[k] < thr)) cand |= 1u << k;      // NaN threshold or value: candidate
+        if ((GJKEPA_PAD_V0 || i < n) && !(sv[k] < thr)) cand |= 1u << k;      // NaN threshold or value: candidate
     }
     if constexpr (GJKEPA_SCREEN_SINGLE) {
         // one candidate in the whole group (the usual case): it is the fp64 argmax, so its index is
@@ -346,6 +348,19 @@ CTX_T DEV void screened_idx(const CTX& c, V3<T> d, int h, float vmax, int& out) 
 // max scans (:381, :401, :471-472) for the same direction.
 template <typename T, int K> struct DotSet { T t[2][K]; T m[2]; };
 
+// GJKEPA_PAD_V0: the hull slots past a hull's count hold copies of its vertex 0 (load_hulls), whose dot
+// can tie only with vertex 0 itself at a higher index, so the lowest-index argmax and the maxima are the
+// plain scan's without masking the padding (three VALU per vertex and hull); the contact band sets,
+// which count members, still mask by index.
+CTX_T DEV T dot_slot(int i, int n, T t) {
+    if constexpr (GJKEPA_PAD_V0) return t;
+    else return i < n ? t : -Tol<T>::BIG;
+}
+// this lane's running maximum of the dots: v_max_f64 (red_max) instead of compare + two selects
+template <typename T> DEV T dots_max(T t, T v) {
+    if constexpr (GJKEPA_DOTS_FMAX) return red_max(t, v);
+    else return t > v ? t : v;
+}
 CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int& ib) {
     T (&ta)[K] = D.t[0];
     T (&tb)[K] = D.t[1];
@@ -355,26 +370,26 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
         const V3<T> a = c.AV(k);
-        ta[k] = i < c.na ? d.x * a.x + d.y * a.y + d.z * a.z : -Tol<T>::BIG;
-        va = ta[k] > va ? ta[k] : va;
+        ta[k] = dot_slot<T, TH, G, K, VC, FC, LH>(i, c.na, d.x * a.x + d.y * a.y + d.z * a.z);
+        va = dots_max(ta[k], va);
     }
     gk_lds_fence();                      // hull B's vertices are read after hull A's dots
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
         const V3<T> b = c.BV(k);
-        tb[k] = i < c.nb ? -(d.x * b.x + d.y * b.y + d.z * b.z) : -Tol<T>::BIG;
-        vb = tb[k] > vb ? tb[k] : vb;
+        tb[k] = dot_slot<T, TH, G, K, VC, FC, LH>(i, c.nb, -(d.x * b.x + d.y * b.y + d.z * b.z));
+        vb = dots_max(tb[k], vb);
     }
     } else {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = k * G + c.g.gl;
         const V3<T> a = c.AV(k), b = c.BV(k);
-        ta[k] = i < c.na ? d.x * a.x + d.y * a.y + d.z * a.z : -Tol<T>::BIG;
-        tb[k] = i < c.nb ? -(d.x * b.x + d.y * b.y + d.z * b.z) : -Tol<T>::BIG;
-        va = ta[k] > va ? ta[k] : va;
-        vb = tb[k] > vb ? tb[k] : vb;
+        ta[k] = dot_slot<T, TH, G, K, VC, FC, LH>(i, c.na, d.x * a.x + d.y * a.y + d.z * a.z);
+        tb[k] = dot_slot<T, TH, G, K, VC, FC, LH>(i, c.nb, -(d.x * b.x + d.y * b.y + d.z * b.z));
+        va = dots_max(ta[k], va);
+        vb = dots_max(tb[k], vb);
     }
     }
     va = gmax<G>(va);
@@ -2035,8 +2050,10 @@ CTX_T DEV bool load_hulls(CTX& c, const TH* __restrict__ pa, const TH* __restric
     for (int k = 0; k < K; ++k) {
         const int i = k * G + gl;
         TH ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
-        if (i < c.na) { ax = pa[i]; ay = pa[c.na + i]; az = pa[2 * c.na + i]; }
-        if (i < c.nb) { bx = pb[i]; by = pb[c.nb + i]; bz = pb[2 * c.nb + i]; }
+        // slots past the count: zeros, or vertex 0 again (GJKEPA_PAD_V0, support_dots)
+        const int ja = i < c.na ? i : 0, jb = i < c.nb ? i : 0;
+        if (i < c.na || (GJKEPA_PAD_V0 && c.na > 0)) { ax = pa[ja]; ay = pa[c.na + ja]; az = pa[2 * c.na + ja]; }
+        if (i < c.nb || (GJKEPA_PAD_V0 && c.nb > 0)) { bx = pb[jb]; by = pb[c.nb + jb]; bz = pb[2 * c.nb + jb]; }
         nonfinite = nonfinite || !isfinite(ax) || !isfinite(ay) || !isfinite(az) || !isfinite(bx) ||
                     !isfinite(by) || !isfinite(bz);
         if constexpr (kScreen) {
