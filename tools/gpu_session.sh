@@ -16,6 +16,7 @@
 #   hull           convex-hull module: its GPU tests, H1-H3 bench lines, rocprofv3 of H1
 #   scene          broad phase + narrow phase scene bench and its rocprofv3 kernel statistics
 #   svc            resident query service: concurrent-batch cost (tools/svc_concurrent.py)
+#   c5sweep        config C5's fp64 / fp32 sweep with the >= 64-face subset (tools/c5_sweep.py)
 #   svcprobe       lone-caller latency (tools/svc_probe.py) of the product build and, from the stamps
 #                  build (build/diag/stamps), the serving wave's time per phase
 # Results land in gpurun_out/TAG; tools/collect.sh copies them into profiles/.
@@ -98,6 +99,7 @@ step_scene() {
   timeout -k 10 300 python tools/bench_scene.py > $OUT/scene.json 2> $OUT/scene.err && cat $OUT/scene.json && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_scene -o run --output-format csv -- python3 tools/bench_scene.py --no-cpu > $OUT/prof_scene.json 2> $OUT/prof_scene.err
 }
+step_c5sweep() { timeout -k 10 500 python tools/c5_sweep.py $((1 << 20)) $OUT/c5_fp32_sweep.json > $OUT/c5_sweep.log 2>&1 && tail -n 3 $OUT/c5_sweep.log; }
 step_svcprobe() {
   GJKEPA_QUERY_STATS=1 timeout -k 10 300 python tools/svc_probe.py 3000 > $OUT/svc_probe.txt 2>&1 && cat $OUT/svc_probe.txt && \
   GJKEPA_LIB=$D/diag/stamps/libgjkepa_hip.so timeout -k 10 300 python tools/svc_probe.py 3000 > $OUT/svc_probe_stamps.txt 2>&1 && cat $OUT/svc_probe_stamps.txt
