@@ -50,15 +50,6 @@ constexpr int ST_PARKED = 104;  // internal: polytope parked for the next tier (
 // dot products, and for hull B while hull A's are still live, which is where most of the GJK / EPA
 // tiers' register peaks and scratch spills came from.
 DEV void gk_lds_fence() { asm volatile("" ::: "memory"); }
-#ifndef GJKEPA_ARGIDX_MIN
-#define GJKEPA_ARGIDX_MIN 0       // support_dots' argmax index by an int group min over the lanes' lowest matching slots (A/B)
-#endif
-#ifndef GJKEPA_VIS_OWN
-#define GJKEPA_VIS_OWN 1          // hull_add's visible list tests the lane's own visibility, not its bit of the group ballot
-#endif
-#ifndef GJKEPA_ARGMIN_WIN
-#define GJKEPA_ARGMIN_WIN 1       // face_argmin's winner as a lane predicate (no second ballot)
-#endif
 // Per group width: the small-hull tiers (G < 32) lose by a fence (the hoisted loads are their memory-level
 // parallelism: C2 -3 to -4% in round 5), the wide large-hull tiers spill without one.  A/B r6 (2 rounds):
 // GJK tier 2's screen fenced (65 -> 14 spilled VGPRs) C4 42.55 -> 42.90; with EPA tier 3's dots too (52 -> 0)
@@ -403,23 +394,6 @@ CTX_T DEV void support_dots(const CTX& c, V3<T> d, DotSet<T, K>& D, int& ia, int
     }
     va = gmax<G>(va);
     vb = gmax<G>(vb);
-    if constexpr (GJKEPA_ARGIDX_MIN) {
-        // lowest index holding the maximum: this lane's lowest matching slot, then an int group min
-        int xa = 0x7FFFFFFF, xb = 0x7FFFFFFF;
-#pragma unroll
-        for (int k = K - 1; k >= 0; --k) {
-            const int i = k * G + c.g.gl;
-            xa = ta[k] == va ? i : xa;
-            xb = tb[k] == vb ? i : xb;
-        }
-        xa = gmin<G>(xa);
-        xb = gmin<G>(xb);
-        ia = c.g.uni(xa == 0x7FFFFFFF ? 0 : xa);
-        ib = c.g.uni(xb == 0x7FFFFFFF ? 0 : xb);
-        D.m[0] = va;
-        D.m[1] = vb;
-        return;
-    }
     const int sh = c.g.lane & ~(G - 1);
     int xa = -1, xb = -1;
 #pragma unroll
@@ -561,19 +535,18 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
     auto& E = c.L.u.e;
     const int gl = c.g.gl;
     uint64_t vm[R];
-    bool vis[R];             // this lane's face of row r is visible (its own bit of vm[r])
     bool live[R];            // some face of this row is valid somewhere in the wave
     int nvis = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const bool valid = !(F.fv[r] & kEmpty);
-        vis[r] = false;
+        bool vis = false;
         live[r] = __ballot(valid) != 0;
         if (live[r]) {
             // signed distance of p above the face plane: n.p - n.v0 = dot(p, n) + DIST_PF_SIGN(O, face)
-            vis[r] = valid && dot(p, vmk<T>(F.nx[r], F.ny[r], F.nz[r])) + F.d[r] > Tol<T>::HULL;
+            vis = valid && dot(p, vmk<T>(F.nx[r], F.ny[r], F.nz[r])) + F.d[r] > Tol<T>::HULL;
         }
-        vm[r] = c.g.ballot(vis[r]);
+        vm[r] = c.g.ballot(vis);
         nvis += popc(vm[r]);
     }
     nvis = c.g.uni(nvis);
@@ -594,7 +567,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
         for (int r = 0; r < R; ++r) {
             vp[r] = -1;
             if (!live[r]) continue;
-            if (GJKEPA_VIS_OWN ? vis[r] : c.g.bit(vm[r])) {
+            if (c.g.bit(vm[r])) {
                 vp[r] = base + mbcnt(vm[r]);
                 // GJKEPA_HORIZON_W16: v0 repeated in byte 3, so the face's three directed edges are
                 // the 16-bit windows at bytes 0, 1 and 2 (v0v1, v1v2, v2v0)
@@ -626,12 +599,11 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             if constexpr (GJKEPA_HORIZON_W16) {
                 // the twin (w, u) is a directed edge of face j iff it is one of its three 16-bit windows
                 const uint32_t t = w | (u << 8);
-                const uint2* vl = reinterpret_cast<const uint2*>(E.x.h.visl);   // (ids, key) word pairs
                 for (int j = 0; j < nvis; ++j) {
-                    const uint2 qj = vl[j];
-                    const uint32_t q = qj.x;
+                    const uint64_t qj = E.x.h.visl[j];
+                    const uint32_t q = (uint32_t)qj;
                     twin = twin || (q & 0xffffu) == t || ((q >> 8) & 0xffffu) == t || (q >> 16) == t;
-                    rank += qj.y < kk ? 1 : 0;
+                    rank += (uint32_t)(qj >> 32) < kk;
                 }
             } else {
                 for (int j = 0; j < nvis; ++j) {
@@ -856,21 +828,12 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& ne
     }
     const T vmin = gmin<G>(v);
     const bool tie = rr >= 0 && v == vmin;
-    bool win = tie;                                      // face keys are unique: one lane wins
-    if constexpr (GJKEPA_ARGMIN_WIN) {
-        if (c.g.unib(popc(c.g.ballot(tie)) > 1)) {
-            const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
-            win = tie && kk == kmin;
-        }
-    } else {
-        uint64_t m = c.g.ballot(tie);
-        if (c.g.unib(popc(m) > 1)) {
-            const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
-            m = c.g.ballot(tie && kk == kmin);
-        }
-        win = c.g.bit(m);
+    uint64_t m = c.g.ballot(tie);
+    if (c.g.unib(popc(m) > 1)) {
+        const uint32_t kmin = (uint32_t)gmin<G>((int)(tie ? kk : 0x7FFFFFFFu));
+        m = c.g.ballot(tie && kk == kmin);
     }
-    if (win) {
+    if (c.g.bit(m)) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (rr == r) {
