@@ -353,8 +353,17 @@ def run_leg(cfg: str, args, dev, stream, prec: int, lib_src: str) -> dict:
          "status_counts": {int(k): int(v) for k, v in zip(*np.unique(recs["status"], return_counts=True))},
          "dominant_kernel": dominant_kernel(lt, read_tally(ws), recs, bpq, pmc_entry(args.precision, cfg, n, lib_src))}
     pmc = pmc_entry(args.precision, cfg, n, lib_src)
-    if pmc:
-        r["traffic_per_chain"] = pmc["bytes_per_launch"]
+    dom = r["dominant_kernel"]
+    # the leg's own roofline block, as the main line's: the dominant kernel's achieved bytes against
+    # the HBM peak, its PMC traffic per launch, and the chain's traffic / VALU issue from the same run
+    r["roofline"] = {"bound": "hbm", "achieved": dom["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": dom["frac"], "traffic": dom.get("pmc", {}).get("traffic_per_launch"),
+                     "kernel": dom["kernel"], "pmc_src": pmc["src"] if pmc else None}
+    r["traffic_per_chain"] = pmc["bytes_per_launch"] if pmc else None
+    r["valu_issue"] = ({"instr_per_query": round(pmc["valu_instr_per_query"], 1),
+                        "issue_frac_pmc": round(pmc["valu_issue_frac"], 4),
+                        "busy_frac_pmc": round(pmc["valu_busy_frac"], 4) if pmc.get("valu_busy_frac") else None}
+                       if pmc else None)
     if prec == gjkepa.PREC_F64 and args.leg_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # checker only, after the timed steps
