@@ -838,7 +838,8 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& ne
         for (int r = 0; r < R; ++r)
             if (rr == r) {
                 E.best[0] = F.nx[r]; E.best[1] = F.ny[r]; E.best[2] = F.nz[r];
-                E.bestv = (F.fv[r] & 0xffu) | (F.d[r] < T(0) ? 0x80000000u : 0u);
+                // fp32: all three vertex ids (the certificate's normal bound reads them); fp64: the first
+                E.bestv = (F.fv[r] & (certify<T>() ? 0xffffffu : 0xffu)) | (F.d[r] < T(0) ? 0x80000000u : 0u);
             }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1120,7 +1121,15 @@ CTX_T DEV int epa_close(CTX& c, EPAST_T& S, T& depth, V3<T>& normal) {
 #pragma unroll
             for (int r = 0; r < R; ++r) out = out || (!(S.F.fv[r] & kEmpty) && !(S.F.d[r] < T(0)));
             const float sc = c.vmax_a + c.vmax_b;
-            if (c.g.any(out) || c.g.unib(!(S.hsup - S.minv + Tol<T>::CERT_NOISE * sc <= Tol<T>::CERT_GAP * S.minv)))
+            // the final face's normal rounding bound (Tol<float>::CERT_ANGLE), from its vertices
+            const uint32_t bw = c.L.u.e.bestv;
+            const V3<T> U = c.vert((int)(bw & 0xffu)), W = c.vert((int)((bw >> 8) & 0xffu)), P = c.vert((int)((bw >> 16) & 0xffu));
+            const V3<T> e1 = vsub(W, U), e2 = vsub(P, W);
+            const T l1 = norm2(e1), l2 = norm2(e2), lc = norm2(cross(e1, e2));
+            const T u = T(5.9604644775390625e-08), k = T(3.4641016151377544), three = T(3), two = T(2);
+            const T th = ((((k * u) * sc) * (l1 + l2)) + (((three * u) * l1) * l2)) / lc + two * u;
+            if (c.g.any(out) || c.g.unib(!(S.hsup - S.minv + Tol<T>::CERT_NOISE * sc <= Tol<T>::CERT_GAP * S.minv)) ||
+                c.g.unib(!(th <= Tol<T>::CERT_ANGLE)))
                 return ST_REDO;
         }
     }

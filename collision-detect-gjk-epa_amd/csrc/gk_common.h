@@ -46,6 +46,12 @@ template <> struct Tol<float> {              // fp32 throughput path: tolerances
     static constexpr float CERT_DROP = 5.0e-7f;
     static constexpr float CERT_GAP = 5.0e-7f;
     static constexpr float CERT_NOISE = 2.384185791015625e-07f;   // 4 x 2^-24
+    // and the final face's unit normal: its fp32 rounding error, bounded from the face's edges e1, e2 by
+    // (2 sqrt3 u (|A| + |B|) (|e1| + |e2|) + 3 u |e1| |e2|) / |e1 x e2| + 2 u (u = 2^-24: the Minkowski
+    // points' coordinate error propagated through the cross product, then the normalisation), must stay
+    // within CERT_ANGLE radians, half the gate's 1e-5 (CPU model sweep, 65,536 pairs: C5's largest non-tie
+    // angle 3.4e-6 -> 1.1e-6 rad, 0.3% -> 2.3% of its pairs recomputed; C2 / C4 +0.2 / +1.9 points)
+    static constexpr float CERT_ANGLE = 5.0e-6f;
 };
 
 DEV double tsqrt(double x) { return ::sqrt(x); }

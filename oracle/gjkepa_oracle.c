@@ -353,7 +353,11 @@ int oracle_epa_trace = 0;
  * support gap h_M(n) - depth at termination plus the fp32 evaluation noise of both terms
  * (oracle_cert_noise x (|A| + |B|), |A| the largest |coordinate| of hull A), relative to the depth. */
 double oracle_cert_drop = 5e-7, oracle_cert_gap = 5e-7, oracle_cert_noise = 2.384185791015625e-07;   /* 4 x 2^-24 */
-static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: origin not inside */
+/* and the largest rounding error of the final face's unit normal (radians), bounded from its edges:
+ * (2 sqrt3 u (|A|+|B|) (|e1|+|e2|) + 3 u |e1||e2|) / |e1 x e2| + 2u, u = 2^-24 */
+double oracle_cert_angle = 5e-6;
+static _Thread_local int g_cert;     /* bit 0: MINLOC drop, bit 1: termination gap, bit 3: origin not inside,
+                                        bit 4: normal rounding bound */
 static _Thread_local double g_cert_scale;   /* max |coordinate| of A + that of B */
 #include <stdio.h>
 
@@ -462,6 +466,13 @@ static int epa(const hull_t* A, const hull_t* B, const v3* S, hullbuf* H,
                 int out = 0;
                 for (int f = 0; f < F2; ++f) out |= !(H->f[f].sd < 0.0);
                 if (out) g_cert |= 8;
+                const v3 U = H->vert[H->f[ml2].v[0]], W = H->vert[H->f[ml2].v[1]], P = H->vert[H->f[ml2].v[2]];
+                const v3 e1 = vsub(W, U), e2 = vsub(P, W), cr = cross(e1, e2);
+                /* every operand a variable of the narrow phase's type: the same fp32 operations as the kernel */
+                const double l1 = norm2(e1), l2 = norm2(e2), lc = norm2(cr), u = 5.9604644775390625e-08,
+                             k = 3.4641016151377544, three = 3.0, two = 2.0;
+                const double th = ((((k * u) * g_cert_scale) * (l1 + l2)) + (((three * u) * l1) * l2)) / lc + two * u;
+                if (!(th <= oracle_cert_angle)) g_cert |= 16;
             }
         }
         if (stop) { *depth = minv2; *normal = dir2; return 0; }

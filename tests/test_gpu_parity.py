@@ -181,3 +181,24 @@ def test_fp32_tolerance_sweep(cfg):
     rep = fp32_report(pool, g, r)
     assert passes(rep), (cfg, rep)
     assert rep["depth_err_over_max1d_max"] <= 1e-6 and rep["normal_angle_rad_p999"] < 1e-5, (cfg, rep)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C5", "C4"])
+def test_fp32_records_equal_cpu_model(cfg):
+    """fp32 parity, exact: the GPU's fp32 records on 32,768 pairs of each config equal the
+    CPU model of the path byte for byte — the fp32 build of the oracle, its uncertified pairs (the same
+    certificate: relative support gap with the fp32 noise term, MINLOC drop, origin inside, the final
+    normal's rounding bound) replaced by the fp64 oracle's records rounded to fp32."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import oracle
+    from bench import CONFIGS, SEED
+    from fp32_check import model_fp32
+    nmin, nmax, rmax, _, _ = CONFIGS[cfg]
+    n = 32768
+    pool = gjkepa.synth_pairs(SEED, n, nmin, nmax, rmax)
+    g = gjkepa.gjkepa_batch(pool, 2, 1.0, precision=gjkepa.PREC_F32)
+    r64 = oracle.gjkepa_batch(pool, 2, 1.0, 16)
+    m, redo = model_fp32(pool, r64, 16)
+    eq = (g.view(np.uint8).reshape(n, -1) == m.view(np.uint8).reshape(n, -1)).all(axis=1)
+    assert eq.all(), (cfg, int((~eq).sum()), np.nonzero(~eq)[0][:8].tolist(), int(redo.sum()))

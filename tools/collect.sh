@@ -30,4 +30,8 @@ for c in C2 C4 C5; do
   fi
 done
 for t in 1 16; do [ -f $S/callpattern_$t.txt ] && cp $S/callpattern_$t.txt $DEST/callpattern_${t}_src$SRC.txt; done
+[ -f $S/c5_fp32_sweep.json ] && cp $S/c5_fp32_sweep.json $DEST/c5_fp32_sweep_src$SRC.json
+[ -f $S/svc_concurrent.json ] && cp $S/svc_concurrent.json $DEST/svc_concurrent_src$SRC.json
+[ -f $S/bench_2rank_gloo.json ] && cp $S/bench_2rank_gloo.json $DEST/bench_2rank_gloo_src$SRC.json
+[ -f $S/svc_probe.txt ] && cp $S/svc_probe.txt $DEST/svc_probe_src$SRC.txt
 echo "collected $S -> $DEST"
