@@ -48,24 +48,27 @@ class RecordExchange:
     the records are gathered through host memory, in line.  `drain()` waits for every gather."""
 
     def __init__(self, nbytes: int, world: int, rank: int, device, precision: int, comm: gjkepa.Comm | None = None,
-                 nbuf: int = 2, group=None):
+                 nbuf: int = 2, group=None, device_group=None):
         import torch
 
         self.world, self.rank, self.group, self.comm = world, rank, group, comm
+        # device_group: a torch.distributed "nccl" (RCCL) process group, the device-to-device exchange when
+        # the library's communicator is not available (same overlapped, double-buffered schedule)
+        self.device_group = device_group if comm is None else None
         self.precision = precision
         self.nbytes = nbytes
         self.count = nbytes // gjkepa.load().gjkepa_record_bytes(precision)
-        k = nbuf if comm is not None else 1
+        k = nbuf if self.overlap else 1
         self.gathered = [torch.zeros(world * nbytes, dtype=torch.uint8, device=device) for _ in range(k)]
         self.local = [g[rank * nbytes:(rank + 1) * nbytes] for g in self.gathered]
-        self.stream = torch.cuda.Stream(device=device) if comm is not None else None
+        self.stream = torch.cuda.Stream(device=device) if self.overlap else None
         self.done = [None] * k
         self.steps = 0
         self.cur = 0
 
     @property
     def overlap(self) -> bool:
-        return self.comm is not None
+        return self.comm is not None or self.device_group is not None
 
     def buffer(self, stream=None):
         b = self.steps % len(self.local)
@@ -80,7 +83,7 @@ class RecordExchange:
 
         b = self.cur
         self.steps += 1
-        if self.comm is None:                   # gloo rehearsal: host-staged
+        if not self.overlap:                    # gloo rehearsal: host-staged
             g = torch.empty(self.gathered[b].numel(), dtype=torch.uint8)
             dist.all_gather_into_tensor(g, self.local[b].cpu(), group=self.group)
             self.gathered[b].copy_(g)
@@ -88,8 +91,12 @@ class RecordExchange:
         ready = torch.cuda.Event()
         ready.record(stream)
         self.stream.wait_event(ready)
-        self.comm.allgather_records(self.precision, self.local[b].data_ptr(), self.gathered[b].data_ptr(),
-                                    self.count, self.stream.cuda_stream)
+        if self.comm is not None:
+            self.comm.allgather_records(self.precision, self.local[b].data_ptr(), self.gathered[b].data_ptr(),
+                                        self.count, self.stream.cuda_stream)
+        else:
+            with torch.cuda.stream(self.stream):
+                dist.all_gather_into_tensor(self.gathered[b], self.local[b], group=self.device_group)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         self.done[b] = ev

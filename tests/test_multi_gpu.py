@@ -7,7 +7,9 @@
   one GPU, so the lists repeat device 0 (2, 3 and 8 shards): every shard still goes through the
   shard / hull-range rebase / per-shard thread path, and the shards of one device run in turn.
 - The library's RCCL communicator (world 1 here; the driver's 8-GPU run exercises world 8): the
-  in-place and out-of-place all-gather of records returns them unchanged.
+  in-place and out-of-place all-gather of records returns them unchanged; shard.RecordExchange's
+  overlapped, double-buffered gather over it, and over the torch.distributed "nccl" (RCCL) group that
+  bench.py falls back to when the library's communicator cannot start.
 - Config C3 whole: the 2^24-pair job as 8 ranks of bench.py (torch.distributed.run, one process per
   rank, all on this box's GPU, host-staged gather), then in this process the same 2^24 pairs as one
   contiguous gjkepa_batch and as gjkepa_batch_multi over 8 shards of device 0: every rank's slot of the
@@ -165,6 +167,51 @@ def test_record_exchange_rccl_overlapped_steps():
         assert ex.gathered[1].cpu().numpy().tobytes() == refs[3].tobytes()
     finally:
         comm.close()
+
+
+_TORCH_RCCL_SCRIPT = r"""
+import sys, numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+import gjkepa, shard
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[2], world_size=1, rank=0)
+g = dist.new_group(backend="nccl")
+dev = torch.device("cuda", 0)
+n, prec = 1 << 15, gjkepa.PREC_F64
+rb = gjkepa.load().gjkepa_record_bytes(prec)
+ex = shard.RecordExchange(n * rb, 1, 0, dev, prec, comm=None, device_group=g)
+assert ex.overlap and len(ex.gathered) == 2
+wsb = gjkepa.workspace_bytes_for(n, 0)
+ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+st = torch.cuda.current_stream(dev)
+for i in range(3):
+    pool = gjkepa.synth_pairs(0x6A4B5C1D + 31 * i, n, 32, 32, 2.5)
+    ref = gjkepa.gjkepa_batch(pool, 2, 1.0)
+    v, o, c, p = (torch.from_numpy(a).to(dev) for a in (pool.verts, pool.hull_off, pool.hull_cnt, pool.pairs.reshape(-1)))
+    buf = ex.buffer(st)
+    gjkepa.gjkepa_batch_device(2, 1.0, gjkepa.DTYPE_F32, prec, v.data_ptr(), o.data_ptr(), c.data_ptr(), p.data_ptr(),
+                               n, buf.data_ptr(), ws.data_ptr(), wsb, st.cuda_stream)
+    ex.submit(st)
+    torch.cuda.synchronize(dev)
+    assert ex.last_gathered.cpu().numpy().tobytes() == ref.tobytes(), i
+ex.drain()
+dist.destroy_process_group()
+print("ok")
+"""
+
+
+def test_record_exchange_torch_rccl_group(tmp_path):
+    """The fallback bench.py takes when the library's RCCL communicator cannot start: the same overlapped,
+    double-buffered exchange through a torch.distributed "nccl" (RCCL) process group, device to device.
+    World 1 in a fresh process (one GPU here); three steps of gjkepa_batch_device, each step's gathered
+    records equal to that step's."""
+    import subprocess
+    import sys
+    pkg = os.path.join(ROOT, "collision-detect-gjk-epa_amd")
+    f = tmp_path / "rccl_group.py"
+    f.write_text(_TORCH_RCCL_SCRIPT)
+    p = subprocess.run([sys.executable, str(f), pkg, "29557"], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), (p.stdout[-2000:], p.stderr[-3000:])
 
 
 def test_two_rank_bench_verifies_its_exchange(tmp_path):
