@@ -52,7 +52,9 @@ def fp32_report(pool, g, r, angle: float | None = None) -> dict:
     ang = np.where(both, np.arccos(np.clip(cos, -1.0, 1.0)), 0.0)
     unit = ad / np.maximum(1.0, np.abs(d64))
     depth_bad = both & (ad > DEPTH_TOL * np.abs(d64))
-    wide = np.nonzero(ang > angle)[0]
+    # every pair whose normal is off by more than a tenth of the bound is checked for a tie, so the
+    # reported non-tie maximum is one (a tie 0.9 x the bound apart would otherwise count as a non-tie)
+    wide = np.nonzero(ang > 0.1 * angle)[0]
     gaps = support_gap(pool, wide, a[wide], d64[wide]) if wide.size else np.zeros(0)
     tie = gaps <= TIE_REL * np.abs(d64[wide])
     ang_nontie = ang.copy()
@@ -67,8 +69,9 @@ def fp32_report(pool, g, r, angle: float | None = None) -> dict:
         "depth_out_of_tol": int(depth_bad.sum()),
         "normal_angle_rad_p999": q(ang, 0.999), "normal_angle_rad_max": float(ang.max()),
         "normal_angle_rad_max_nontie": float(ang_nontie.max()),
-        "normal_ties": int(tie.sum()), "normal_tie_gap_max": float(gaps.max()) if gaps.size else 0.0,
-        "normal_out_of_tol": int((~tie).sum()),
+        "normal_ties": int((tie & (ang[wide] > angle)).sum()),
+        "normal_tie_gap_max": float(gaps[tie].max()) if tie.any() else 0.0,
+        "normal_out_of_tol": int((~tie & (ang[wide] > angle)).sum()),
         "gate": {"depth": f"|d32-d64| <= {DEPTH_TOL} |d64|",
                  "normal": f"angle <= {angle} rad, or h_M(n32) - d64 <= {TIE_REL} |d64| (tie)"},
     }
