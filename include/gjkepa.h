@@ -59,7 +59,8 @@ extern "C" {
 #define GJKEPA_DTYPE_F32 0      /* vertex storage dtype */
 #define GJKEPA_DTYPE_F64 1
 #define GJKEPA_PREC_F64  1      /* compute precision: fp64 = the reference's REAL*8 semantics */
-#define GJKEPA_PREC_F32  0      /* compute precision: fp32 throughput path (tolerance-swept) */
+#define GJKEPA_PREC_F32  0      /* compute precision: fp32, opt-in; an fp32 answer is kept only when certified to
+                                   1e-6 relative depth (else recomputed in fp64), which makes it slower than F64 */
 
 #define GJKEPA_MAX_HULL_VERTS 256   /* largest hull the kernels accept (config C4: 8..256) */
 

@@ -10,6 +10,7 @@
 #   pmc            PMC passes (one counter group per rocprofv3 run) for C2 / C4 / C5
 #   ab=R:CFGS:V1,V2  A/B of library variants (tools/build_variant.sh) against the in-tree build,
 #                  R interleaved rounds over configs CFGS (comma list), e.g. ab=2:C2,C5:e0x
+#   envab=R:CFGS:VAR=v1,v2  A/B of a run-time environment knob of the in-tree build (e.g. GJKEPA_EPA0_FIRST)
 #   callpattern    Fortran OpenMP loop of single GJKEPA calls vs GJKEPA_BATCH (1 / 16 threads)
 #   stamps=CFGS    per-phase stamps from the diagnostic build (build/diag/stamps)
 #   gloo2          two-rank bench rehearsal over gloo on the one GPU
@@ -71,6 +72,20 @@ step_ab() {
         GJKEPA_LIB=$lib timeout -k 10 240 python bench.py --config $c --legs none --cpu-sample 65536 --no-f32-leg --no-warm-leg --launch-timing off \
           > $OUT/ab_${v}_${c}_$r.json 2>> $OUT/ab.err || { echo "FAIL $v $c"; tail -5 $OUT/ab.err; return 1; }
         echo "$r $v $c $(python3 -c "import json;d=json.loads(open('$OUT/ab_${v}_${c}_$r.json').read().splitlines()[-1]);print(d['value'], d['ms_per_step'], d.get('parity_sample',{}).get('all_equal'))")"
+      done
+    done
+  done
+}
+step_envab() {
+  local rounds=${1%%:*} rest=${1#*:}
+  local cfgs=${rest%%:*} kv=${rest#*:}
+  local var=${kv%%=*} vals=${kv#*=}
+  for r in $(seq 1 $rounds); do
+    for v in ${vals//,/ }; do
+      for c in ${cfgs//,/ }; do
+        env $var=$v timeout -k 10 240 python bench.py --config $c --legs none --cpu-sample 65536 --no-f32-leg --no-warm-leg --launch-timing off \
+          > $OUT/envab_${v}_${c}_$r.json 2>> $OUT/envab.err || { echo "FAIL $var=$v $c"; tail -5 $OUT/envab.err; return 1; }
+        echo "$r $var=$v $c $(python3 -c "import json;d=json.loads(open('$OUT/envab_${v}_${c}_$r.json').read().splitlines()[-1]);print(d['value'], d['ms_per_step'], d.get('parity_sample',{}).get('all_equal'))")"
       done
     done
   done
