@@ -198,6 +198,10 @@
 #define GJKEPA_PAD_V0 1             // hull slots past the count hold vertex 0 again; support scans skip the mask
                                     // (A/B r6, 3 rounds: C2 +1.1%, C4 +1.6%, C5 +1.9%; 0: masked)
 #endif
+#ifndef GJKEPA_EMPTY_INF
+#define GJKEPA_EMPTY_INF 1          // free polytope face slots carry a -inf distance; MINLOC without validity masks
+                                    // (A/B r6, 3 rounds: C2 +3.4%, C4 +1.7%, C5 +2.7%; 0: masked scan)
+#endif
 #ifndef GJKEPA_DOTS_FMAX
 #define GJKEPA_DOTS_FMAX 1          // support_dots' per-lane maximum on v_max_f64 (0: compare + selects, A/B)
 #endif

@@ -522,6 +522,13 @@ template <typename T, int R> struct Faces {
 };
 #define FACES_T Faces<T, (FC + G - 1) / G>
 
+// A free slot: kEmpty, and with GJKEPA_EMPTY_INF a distance of -inf, so that |d| = +inf never wins MINLOC
+// and dot(p, n) + d never passes the visibility test: the MINLOC scan needs no validity mask
+template <typename T, int R> DEV void free_slot(Faces<T, R>& F, int r) {
+    F.fv[r] = kEmpty;
+    if constexpr (GJKEPA_EMPTY_INF) F.d[r] = -__builtin_inf();
+}
+
 template <typename T> DEV T qnan() { return __builtin_nan(""); }
 
 // Add point p (vertex id k; appended at nv when `append`): faces it sees (signed distance >
@@ -652,7 +659,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
     bool bad = false;
 #pragma unroll
     for (int r = 0; r < R; ++r)
-        if (vp[r] >= 0) F.fv[r] = kEmpty;
+        if (vp[r] >= 0) free_slot(F, r);
     int top = 0;
     for (int placed = 0; placed < nh;) {
         int row = -1;
@@ -698,7 +705,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             int h = vp[r];
             if (h < 0 && slot >= hw && slot < hw + app) h = nvis + slot - hw;
             tj[r] = h < nh ? h : -1;
-            if (vp[r] >= 0) F.fv[r] = kEmpty;
+            if (vp[r] >= 0) free_slot(F, r);
         }
         if (app > 0) hw += app;
     } else {
@@ -712,7 +719,7 @@ CTX_T DEV int hull_add(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, in
             fbase += popc(fm);
             tj[r] = fre && fr < nh ? fr : -1;
             if (tj[r] >= 0) top = r * G + gl + 1;
-            if (vis) F.fv[r] = kEmpty;
+            if (vis) free_slot(F, r);
         }
         top = gmax<G>(top);
         hw = hw > top ? hw : top;
@@ -782,7 +789,7 @@ CTX_T DEV int hull_build(CTX& c, FACES_T& F, uint32_t& kbase, int& hw, int& nv, 
     const int gl = c.g.gl;
     bool bad = false;
 #pragma unroll
-    for (int r = 0; r < R; ++r) F.fv[r] = kEmpty;
+    for (int r = 0; r < R; ++r) free_slot(F, r);
     if (gl < 4) {
         int a = gl == 3 ? i1 : 0, b = (gl == 0 || gl == 2) ? i1 : i2, d = gl == 0 ? i2 : i3;
         V3<T> Pa = vsel(gl == 3, P1, P0);
@@ -819,14 +826,27 @@ CTX_T DEV void face_argmin(CTX& c, const FACES_T& F, T& dmin, V3<T>& n, bool& ne
     T v = Tol<T>::BIG;
     uint32_t kk = 0xFFFFFFFFu;
     int rr = -1;
+    T vmin;
+    if constexpr (GJKEPA_EMPTY_INF) {
+        // free slots hold |d| = +inf: the value-only minimum over every row, then this lane's lowest key
+        // among its rows at the group minimum
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const bool valid = !(F.fv[r] & kEmpty);
-        if (!__ballot(valid)) continue;
-        const T ad = fabs(F.d[r]);
-        if (valid && (ad < v || (ad == v && F.key[r] < kk))) { v = ad; kk = F.key[r]; rr = r; }
+        for (int r = 0; r < R; ++r) v = red_min(fabs(F.d[r]), v);
+        vmin = gmin<G>(v);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (fabs(F.d[r]) == vmin && F.key[r] < kk) { kk = F.key[r]; rr = r; }
+        v = vmin;
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool valid = !(F.fv[r] & kEmpty);
+            if (!__ballot(valid)) continue;
+            const T ad = fabs(F.d[r]);
+            if (valid && (ad < v || (ad == v && F.key[r] < kk))) { v = ad; kk = F.key[r]; rr = r; }
+        }
+        vmin = gmin<G>(v);
     }
-    const T vmin = gmin<G>(v);
     const bool tie = rr >= 0 && v == vmin;
     uint64_t m = c.g.ballot(tie);
     if (c.g.unib(popc(m) > 1)) {
@@ -955,7 +975,7 @@ CTX_T DEV int epa_begin(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> 
     const int gl = c.g.gl;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        S.F.fv[r] = kEmpty;
+        free_slot(S.F, r);
         const int f = r * G + gl;
         if (f < FC) E.dsv[f] = qnan<T>();
     }
@@ -1035,7 +1055,7 @@ CTX_T DEV int epa_seed(CTX& c, EPAST_T& S, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s
     if (!c.g.unib(fabs(dot(vsub(s3, s0), pn)) > Tol<T>::HULL)) return ST_FALLBACK;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        S.F.fv[r] = kEmpty;
+        free_slot(S.F, r);
         const int f = r * G + gl;
         if (f < FC) E.dsv[f] = qnan<T>();
     }
@@ -1264,7 +1284,7 @@ CTX_T DEV void epa_resume(CTX& c, EPAST_T& S, const unsigned char* rec, uint32_t
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int f = r * G + gl;
-        S.F.fv[r] = kEmpty;
+        free_slot(S.F, r);
         if (f < S.hw) {
             const uint32_t w = fv[f];
             if (!(w & kEmpty)) {
