@@ -518,7 +518,7 @@ def main():
 
     bpq = algorithmic_bytes_per_query(float(pool.hull_cnt.sum()) / n, 4, rec_bytes)
     achieved = n * bpq / (kern_ms * 1e-3) / 1e9
-    # HBM traffic and VALU issue of the same chain from the committed PMC run (tools/pmc.sh +
+    # HBM traffic and VALU issue of the same chain from the committed PMC run (tools/gpu_session.sh pmc +
     # tools/pmc_report.py), keyed by precision/config/batch size and stamped with the library's
     # source hash; null unless that hash is the one this process loaded (no figures from another build)
     traffic, valu, pmc_src = None, None, None

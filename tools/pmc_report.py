@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch-chain PMC summary of a tools/pmc.sh run, for bench.py's roofline fields.
+"""Per-launch-chain PMC summary of a PMC run (tools/gpu_session.sh step pmc), for bench.py's roofline fields.
 
 Every kernel of the GJK/EPA/contact chain is dispatched once per bench step; counters are
 averaged over a kernel's dispatches and summed over the chain.  HBM traffic follows
@@ -80,7 +80,7 @@ def main():
         # which a wave had a VALU instruction issuing; against 1024 SIMDs x kernel time x 2.4 GHz
         "valu_busy_frac": tot["SQ_ACTIVE_INST_VALU"] * 4.0 / (1024 * secs * 2.4e9) if secs and tot["SQ_ACTIVE_INST_VALU"] else None,
         "kernels": kernels,
-        "source": f"tools/pmc.sh run {tag}, kernels summed over their dispatches per chain (one chain = one GJK tier-0 dispatch), summed over the chain",
+        "source": f"tools/gpu_session.sh pmc run {tag}, kernels summed over their dispatches per chain (one chain = one GJK tier-0 dispatch), summed over the chain",
     }
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     allj = json.load(open(path)) if os.path.exists(path) else {}
