@@ -1299,10 +1299,12 @@ CTX_T DEV void epa_resume(CTX& c, EPAST_T& S, const unsigned char* rec, uint32_t
     }
 }
 
-// EPA from the simplex (or, with `rec`, from a parked polytope); with `pk`, the polytope is parked
-// (ST_PARKED) when it could outgrow this tier and a park slot is free.
+// EPA from the simplex (or, with `rec`, from a parked polytope); with `park`, the polytope is parked
+// through `pk` (ST_PARKED) when it could outgrow this tier and a park slot is free.  `pk` is passed by
+// value with a flag, not as a maybe-null pointer: a pointer to the caller's copy selected against null
+// keeps that copy in scratch memory (one 32-byte store per lane and pair).
 CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T>& normal, int& iters, int& nf,
-                  const ParkCtl* pk = nullptr, const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
+                  bool park = false, ParkCtl pk = {}, const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
     EPAST_T S;
     int st;
     if (rec) {
@@ -1316,7 +1318,7 @@ CTX_T DEV int epa(CTX& c, V3<T> s0, V3<T> s1, V3<T> s2, V3<T> s3, T& depth, V3<T
         st = epa_close(c, S, depth, normal);
         if (st != ST_CONT) break;
         if constexpr (VC <= GJKEPA_PARK_VC && FC <= GJKEPA_PARK_FC) {
-            if (pk && park_now(c, S, *pk)) { st = ST_PARKED; break; }
+            if (park && park_now(c, S, pk)) { st = ST_PARKED; break; }
         }
         st = epa_grow(c, S, false);
     }
@@ -2022,14 +2024,14 @@ CTX_T DEV int gjk_phase(CTX& c, uint32_t* kc, int& gjk_it, bool try_axis = false
 
 // EPA_solu's polytope loop (:274-323) from the GJK simplex: 0 (depth, n filled), an error
 // status or ST_DEFER; `diag_epa` gets (epa_iters << 8) | (faces << 16).
-CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t& diag_epa, const ParkCtl* pk = nullptr,
-                        const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
+CTX_T DEV int epa_phase(CTX& c, const uint32_t* kc, T& depth, V3<T>& n, uint32_t& diag_epa, bool park = false,
+                        ParkCtl pk = {}, const unsigned char* rec = nullptr, uint32_t* gjk_it = nullptr) {
     V3<T> s0 = zero3<T>(), s1 = s0, s2 = s0, s3 = s0;
     if (!rec) { s0 = decode_pt(c, kc[0]); s1 = decode_pt(c, kc[1]); s2 = decode_pt(c, kc[2]); s3 = decode_pt(c, kc[3]); }
     depth = 0;
     n = zero3<T>();
     int eit = 0, nf = 0;
-    const int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf, pk, rec, gjk_it);
+    const int st = epa(c, s0, s1, s2, s3, depth, n, eit, nf, park, pk, rec, gjk_it);
     diag_epa = ((uint32_t)(eit & 0xff) << 8) | ((uint32_t)(nf & 0xffff) << 16);
     return st;
 }
@@ -2462,7 +2464,7 @@ __global__ __launch_bounds__(64, MINW) void epa_kernel(const gjkepa_epa_args a) 
         const ParkCtl pk{a.park, a.park_ctr, a.park_cap, gjk_it, slot};
         const bool can_park = (PR & 1) && a.park && a.next_code >= 0;
         const int r = (c.na > G * K || c.nb > G * K) ? ST_DEFER
-                    : epa_phase(c, kc, depth, n, de, can_park ? &pk : nullptr,
+                    : epa_phase(c, kc, depth, n, de, can_park, pk,
                                 parked ? a.park + (size_t)(parked - 1) * GJKEPA_PARK_BYTES : nullptr, &it_park);
 #endif
         __builtin_amdgcn_wave_barrier();
