@@ -26,12 +26,15 @@
 #define GJKEPA_G0_MINW 2        // __launch_bounds__ minimum waves per SIMD (caps VGPRs at 512/MINW)
 #endif
 // GJK tier 1: hulls of 33-128 vertices (C5, a quarter of C4); GJK tier 2: up to 256.  A pair goes to
-// the smallest tier that holds its larger hull, so a 128-vertex pair scans 4 vertices per lane, not 8.
+// the smallest tier that holds its larger hull.  Tier 1 runs four pairs per wave at 16 lanes x 8
+// vertices (K = 8 takes the fp32-screened support scan), despite 75 spilled VGPRs at three waves:
+// A/B r6 (2 rounds, profiles/r06/ab_g1_tiers.txt) against 32 x 4 C4 45.76 -> 46.08, C5 25.59 -> 25.97;
+// 64 x 2 lost (C4 -1.2%, C5 -2.9%)
 #ifndef GJKEPA_G1_G
-#define GJKEPA_G1_G 32
+#define GJKEPA_G1_G 16
 #endif
 #ifndef GJKEPA_G1_K
-#define GJKEPA_G1_K 4
+#define GJKEPA_G1_K 8
 #endif
 #ifndef GJKEPA_G1_MINW
 #define GJKEPA_G1_MINW 3
